@@ -1,0 +1,158 @@
+/*
+ * alipmpc.h — C ABI of the MI355X batched ALIP-MPC-CBF footstep planner (libalipmpc.so).
+ *
+ * Drop-in boundary for the reference's per-step NLP solve.  The reference has no C ABI: its planner API
+ * is the Python class MPCCBF (MPC_LIP_modi.py:13-391) whose solveMPCCBF (MPC_LIP_modi.py:197-301)
+ * hands an NLP plugin object LIP_Prob (MPC_LIP_modi.py:394-655: objective / gradient / constraints /
+ * jacobian) to cyipopt.Problem + nlp.solve(u0) (MPC_LIP_modi.py:274-296).  Each entry point below
+ * replaces one of those interfaces for a whole batch of independent instances:
+ *
+ *   alipmpc_solve_batch  <- MPCCBF.select_obs + MPCCBF.solveMPCCBF + cyipopt.Problem.solve, and the
+ *                           rollout of MPCCBF.gen_control_test   (MPC_LIP_modi.py:90-112,197-301,325-338;
+ *                           MPC_LIP_sig_step.py:89-111,184-278; MPC_DD_sig_step.py:70-97,123-193)
+ *   alipmpc_eval_batch   <- LIP_Prob.objective/gradient/constraints/jacobian + the cl/cu/goal set-up
+ *                           of solveMPCCBF                     (MPC_LIP_modi.py:205-271,430-583;
+ *                           MPC_LIP_sig_step.py:195-254,372-496; MPC_DD_sig_step.py:127-141,351-477)
+ *   alipmpc_default_cfg  <- the hard-coded constants of MPCCBF.__init__ / LIP_Prob.__init__
+ *                           (MPC_LIP_modi.py:17-45,397-411; MPC_LIP_sig_step.py:17-44,340-353;
+ *                           MPC_DD_sig_step.py:15-40,323-338)
+ *
+ * Conventions
+ *   - The caller owns every buffer.  hip_stream == NULL: all pointers are HOST pointers; the library
+ *     stages them through its own device workspace and synchronises before returning.
+ *     hip_stream != NULL: all pointers are DEVICE pointers (hipMalloc / torch CUDA tensors) and the call
+ *     is asynchronous on that stream (no host synchronisation, no allocation after the first call of a
+ *     given batch size — graph-capturable).
+ *   - Row-major, instance-major arrays ("B x k" = k contiguous values per instance).
+ *   - Return 0 on success, a negative ALIPMPC_E* code on error; alipmpc_last_error(h) gives the text.
+ *   - There is no CPU execution path: a handle needs a visible gfx950 device.
+ *   - One handle per host thread / stream; distinct handles are independent.
+ *
+ * Problem layout (variant 0 = "modi" MPC_LIP_modi.py, 1 = "sig_step" MPC_LIP_sig_step.py, 2 = "dd"
+ * MPC_DD_sig_step.py):
+ *   LIP (0,1): state x = [px, py, vx, vy, theta] (sdim = 5), decision u = [u_1..u_N], u_i in R^5
+ *              (n = 5N), foothold p_i = W(u_i - A x_i) = [foot x, foot y, turn].
+ *   DD  (2):   state x = [px, py, theta] (sdim = 3), decision u = [v_1, w_1, ..., v_N, w_N] (n = 2N).
+ *   Constraint rows are laid out in a FIXED padded order, rows_per_step rows per step k = 0..N-1:
+ *     LIP: [vbx, vby, circle slot 0..nc_max-1, ellipse slot 0..ne_max-1, leg, dtheta, (f_en if modi)]
+ *     DD : [circle slot 0..nc_max-1, ellipse slot 0..ne_max-1, f_en]
+ *   select_obs (modi) compacts the kept obstacles, in input order, into the first slots; unused slots
+ *   are inactive (row_active = 0, cl = -inf, cu = +inf, value/Jacobian rows = 0).  Dropping the
+ *   inactive rows gives exactly the reference's row order.
+ */
+#ifndef ALIPMPC_H
+#define ALIPMPC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ALIPMPC_VARIANT_MODI 0
+#define ALIPMPC_VARIANT_SIG_STEP 1
+#define ALIPMPC_VARIANT_DD 2
+
+#define ALIPMPC_PREC_FP64 0
+#define ALIPMPC_PREC_FP32 1
+
+/* IPOPT-compatible status codes written to status[] (cyipopt info['status']) */
+#define ALIPMPC_SOLVE_SUCCEEDED 0
+#define ALIPMPC_SOLVED_TO_ACCEPTABLE_LEVEL 1
+#define ALIPMPC_INFEASIBLE_PROBLEM_DETECTED 2
+#define ALIPMPC_MAXIMUM_ITERATIONS_EXCEEDED (-1)
+
+/* error codes */
+#define ALIPMPC_OK 0
+#define ALIPMPC_EINVAL (-1)
+#define ALIPMPC_ENODEV (-2)
+#define ALIPMPC_EHIP (-3)
+#define ALIPMPC_EUNSUPPORTED (-4)
+
+#define ALIPMPC_MAX_N 6      /* horizon limit of the kernels (n = 5N <= 32 -> two 16-column MFMA tiles) */
+#define ALIPMPC_MAX_OBS 16   /* nc_max + ne_max limit */
+
+typedef struct alipmpc_cfg {
+    int32_t N;          /* horizon (reference: step = 3) */
+    int32_t nc_max;     /* circle slots per instance (raw count before select_obs) */
+    int32_t ne_max;     /* ellipse slots per instance */
+    int32_t variant;    /* ALIPMPC_VARIANT_* */
+    int32_t max_iter;   /* interior-point iteration cap */
+    int32_t precision;  /* ALIPMPC_PREC_FP64 / _FP32 (device arithmetic; host buffers stay fp64) */
+    int32_t select_obs; /* 1: MPCCBF.select_obs range filter (modi) */
+    int32_t detour;     /* 1: local-goal detour heuristic of solveMPCCBF (modi, sig_step) */
+    double tol;         /* overall KKT tolerance (IPOPT tol, default 1e-8) */
+    double acceptable_tol;
+    double dt, H, g;    /* step period T, LIP height, gravity */
+    double leg2_max;    /* leg length^2 bound */
+    double bvx_lo, bvx_hi, bvy_lo, bvy_hi; /* body-frame velocity bounds (DD: v bounds in bvx_*) */
+    double dtheta_max;  /* turning bound (DD: omega bound) */
+    double q, p, r;     /* cost weights: position, first-step position, heading */
+    double gamma;       /* D-CBF decay */
+    double s;           /* f_en turning weight */
+    double detect_r2;   /* select_obs range^2 */
+    double dd_t;        /* DD control-smoothness weight */
+    double mu_init;     /* initial barrier parameter */
+} alipmpc_cfg;
+
+/* Fill *out with the reference's constants for a variant and horizon.  nc_max = ne_max = 6,
+ * max_iter = 100, precision fp64. */
+int alipmpc_default_cfg(int32_t variant, int32_t N, alipmpc_cfg* out);
+
+/* Rows per step and total padded rows (m_max) of the fixed constraint layout for cfg. */
+int32_t alipmpc_rows_per_step(const alipmpc_cfg* cfg);
+int32_t alipmpc_num_vars(const alipmpc_cfg* cfg);
+
+/* device: HIP device ordinal (>= 0).  Returns ALIPMPC_ENODEV when no gfx950 device is visible. */
+int alipmpc_create(const alipmpc_cfg* cfg, int device, void** handle);
+
+/*
+ * Solve B independent NLP instances.
+ *   x0    B x sdim         initial state (MPCCBF.gen_control_test `state`)
+ *   goal  B x 2            goal position (MPCCBF `goals`)
+ *   leg   B                od_ev = +-1 (the reference passes -leg_ind)
+ *   cir   B x nc_max x 3   inflated circles [cx, cy, r]   (cir_cbf); nc[b] of them valid
+ *   elp   B x ne_max x 5   inflated ellipses [cx, cy, a, b, phi] (elp_cbf); ne[b] valid (may be NULL if ne_max == 0)
+ *   u0    B x n            initial guess (init_guess)
+ *   last_u B x 2           DD only: previous control (may be NULL otherwise)
+ * Outputs (any output pointer may be NULL except u_out):
+ *   u_out    B x n         solution u
+ *   foot_out B x 3         p_list[0] = W(u_1 - A x0) (LIP) / first control [v, w, 0] (DD)
+ *   x_pred   B x N x sdim  predicted states x_1..x_N (xk_list[1:])
+ *   status   B             IPOPT-compatible status
+ *   iters    B             interior-point iterations used
+ */
+int alipmpc_solve_batch(void* handle, int64_t B,
+                        const double* x0, const double* goal, const int8_t* leg,
+                        const double* cir, const int32_t* nc,
+                        const double* elp, const int32_t* ne,
+                        const double* u0, const double* last_u,
+                        double* u_out, double* foot_out, double* x_pred,
+                        int32_t* status, int32_t* iters,
+                        void* hip_stream);
+
+/*
+ * Evaluate the NLP callbacks and the set-up at given u (parity / oracle hook).  m_max = N*rows_per_step.
+ *   f B, grad B x n, c B x m_max, J B x m_max x n, cl/cu B x m_max, goal_eff B x 2 (after detour),
+ *   row_active B x m_max.  Any output may be NULL.
+ */
+int alipmpc_eval_batch(void* handle, int64_t B,
+                       const double* x0, const double* goal, const int8_t* leg,
+                       const double* cir, const int32_t* nc,
+                       const double* elp, const int32_t* ne,
+                       const double* u, const double* last_u,
+                       double* f, double* grad, double* c, double* J,
+                       double* cl, double* cu, double* goal_eff, int8_t* row_active,
+                       void* hip_stream);
+
+/* Duration in milliseconds of the most recent solve kernel launch on this handle, measured with HIP
+ * events on the launch stream (0 if none). */
+double alipmpc_last_kernel_ms(void* handle);
+
+const char* alipmpc_last_error(void* handle);
+void alipmpc_destroy(void* handle);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ALIPMPC_H */

@@ -1,0 +1,11 @@
+"""alipmpc — MI355X-native batched ALIP-MPC-CBF footstep planner (HIP kernels behind a C ABI).
+
+  Solver       one libalipmpc.so handle: batched solve / eval on host or device buffers
+  default_cfg  the reference's constants per variant (modi / sig_step / dd)
+  planner      MPCCBF drop-in (reference MPC_LIP_modi.MPCCBF signatures) + solve_batch
+"""
+from ._lib import (Cfg, Solver, default_cfg, load, lib_path, num_vars, rows_per_step, EXPORTS, STATUS_NAMES,
+                   VARIANT_MODI, VARIANT_SIG_STEP, VARIANT_DD, PREC_FP64, PREC_FP32)
+
+__all__ = ["Cfg", "Solver", "default_cfg", "load", "lib_path", "num_vars", "rows_per_step", "EXPORTS",
+           "STATUS_NAMES", "VARIANT_MODI", "VARIANT_SIG_STEP", "VARIANT_DD", "PREC_FP64", "PREC_FP32"]

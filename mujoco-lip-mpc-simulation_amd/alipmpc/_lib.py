@@ -1,0 +1,213 @@
+"""ctypes binding of libalipmpc.so (include/alipmpc.h).
+
+This is the reference-side binding a Python caller of the planner would add: plain
+ctypes over the C ABI, numpy arrays for host-pointer calls, torch CUDA tensors (+ the current HIP stream)
+for device-pointer calls.  There is no fallback: if the library or a gfx950 device is missing, the
+calls raise.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from . import build as _build
+
+VARIANT_MODI, VARIANT_SIG_STEP, VARIANT_DD = 0, 1, 2
+PREC_FP64, PREC_FP32 = 0, 1
+
+STATUS_NAMES = {0: "Solve_Succeeded", 1: "Solved_To_Acceptable_Level", 2: "Infeasible_Problem_Detected",
+                -1: "Maximum_Iterations_Exceeded"}
+
+_ERRORS = {-1: "EINVAL", -2: "ENODEV (no visible gfx950 device)", -3: "EHIP", -4: "EUNSUPPORTED"}
+
+
+class Cfg(ctypes.Structure):
+    """alipmpc_cfg"""
+    _fields_ = [(k, ctypes.c_int32) for k in
+                ("N", "nc_max", "ne_max", "variant", "max_iter", "precision", "select_obs", "detour")] + \
+               [(k, ctypes.c_double) for k in
+                ("tol", "acceptable_tol", "dt", "H", "g", "leg2_max", "bvx_lo", "bvx_hi", "bvy_lo", "bvy_hi",
+                 "dtheta_max", "q", "p", "r", "gamma", "s", "detect_r2", "dd_t", "mu_init")]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+EXPORTS = ("alipmpc_default_cfg", "alipmpc_rows_per_step", "alipmpc_num_vars", "alipmpc_create",
+           "alipmpc_solve_batch", "alipmpc_eval_batch", "alipmpc_last_kernel_ms", "alipmpc_last_error",
+           "alipmpc_destroy")
+
+_lib = None
+
+
+def lib_path():
+    return _build.LIB
+
+
+def load(build_if_missing=True):
+    """Load libalipmpc.so (building it in-tree with hipcc if it is missing or stale)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if build_if_missing and _build.needs_build():
+        _build.build()
+    if not os.path.exists(_build.LIB):
+        raise RuntimeError(f"libalipmpc.so not found at {_build.LIB}; run alipmpc.build.build()")
+    L = ctypes.CDLL(_build.LIB)
+    P = ctypes.c_void_p
+    L.alipmpc_default_cfg.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(Cfg)]
+    L.alipmpc_default_cfg.restype = ctypes.c_int
+    L.alipmpc_rows_per_step.argtypes = [ctypes.POINTER(Cfg)]
+    L.alipmpc_rows_per_step.restype = ctypes.c_int32
+    L.alipmpc_num_vars.argtypes = [ctypes.POINTER(Cfg)]
+    L.alipmpc_num_vars.restype = ctypes.c_int32
+    L.alipmpc_create.argtypes = [ctypes.POINTER(Cfg), ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+    L.alipmpc_create.restype = ctypes.c_int
+    L.alipmpc_solve_batch.argtypes = [P, ctypes.c_int64] + [P] * 15
+    L.alipmpc_solve_batch.restype = ctypes.c_int
+    L.alipmpc_eval_batch.argtypes = [P, ctypes.c_int64] + [P] * 18
+    L.alipmpc_eval_batch.restype = ctypes.c_int
+    L.alipmpc_last_kernel_ms.argtypes = [P]
+    L.alipmpc_last_kernel_ms.restype = ctypes.c_double
+    L.alipmpc_last_error.argtypes = [P]
+    L.alipmpc_last_error.restype = ctypes.c_char_p
+    L.alipmpc_destroy.argtypes = [P]
+    L.alipmpc_destroy.restype = None
+    _lib = L
+    return L
+
+
+def default_cfg(variant=VARIANT_MODI, N=3, **overrides):
+    c = Cfg()
+    rc = load().alipmpc_default_cfg(variant, N, ctypes.byref(c))
+    if rc != 0:
+        raise ValueError(f"alipmpc_default_cfg({variant}, {N}) -> {rc}")
+    for k, v in overrides.items():
+        if not hasattr(c, k):
+            raise AttributeError(k)
+        setattr(c, k, v)
+    return c
+
+
+def rows_per_step(cfg):
+    return int(load().alipmpc_rows_per_step(ctypes.byref(cfg)))
+
+
+def num_vars(cfg):
+    return int(load().alipmpc_num_vars(ctypes.byref(cfg)))
+
+
+def _ptr(a):
+    if a is None:
+        return None
+    if hasattr(a, "data_ptr"):          # torch tensor (device mode)
+        return ctypes.c_void_p(a.data_ptr())
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class Solver:
+    """Owns one libalipmpc handle (one config, one device)."""
+
+    def __init__(self, cfg, device=0):
+        self.cfg = cfg
+        self.device = device
+        self._L = load()
+        h = ctypes.c_void_p()
+        rc = self._L.alipmpc_create(ctypes.byref(cfg), device, ctypes.byref(h))
+        if rc != 0:
+            raise RuntimeError(f"alipmpc_create failed: {_ERRORS.get(rc, rc)}")
+        self._h = h
+        self.n = num_vars(cfg)
+        self.rps = rows_per_step(cfg)
+        self.m_max = cfg.N * self.rps
+        self.sdim = 3 if cfg.variant == VARIANT_DD else 5
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.alipmpc_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc != 0:
+            msg = self._L.alipmpc_last_error(self._h).decode()
+            raise RuntimeError(f"{what} failed ({_ERRORS.get(rc, rc)}): {msg}")
+
+    def last_kernel_ms(self):
+        return float(self._L.alipmpc_last_kernel_ms(self._h))
+
+    # ---------------------------------------------------------------- host (numpy) calls
+    def _inputs(self, x0, goal, leg, cir, nc, elp, ne):
+        cfg = self.cfg
+        x0 = np.ascontiguousarray(x0, np.float64).reshape(-1, self.sdim)
+        B = x0.shape[0]
+        goal = np.ascontiguousarray(np.broadcast_to(np.asarray(goal, np.float64), (B, 2)))
+        leg = np.ascontiguousarray(np.broadcast_to(np.asarray(leg), (B,)), np.int8)
+        cir = np.ascontiguousarray(np.broadcast_to(np.asarray(cir, np.float64), (B, cfg.nc_max, 3))) \
+            if cfg.nc_max else np.zeros((B, 0, 3))
+        nc = np.ascontiguousarray(np.broadcast_to(np.asarray(nc), (B,)), np.int32)
+        if cfg.ne_max:
+            elp = np.ascontiguousarray(np.broadcast_to(np.asarray(elp, np.float64), (B, cfg.ne_max, 5)))
+            ne = np.ascontiguousarray(np.broadcast_to(np.asarray(ne), (B,)), np.int32)
+        else:
+            elp, ne = None, None
+        return B, x0, goal, leg, cir, nc, elp, ne
+
+    def solve(self, x0, goal, leg, cir, nc, elp=None, ne=None, u0=None, last_u=None):
+        """Solve a batch from host arrays; returns a dict of numpy outputs."""
+        B, x0, goal, leg, cir, nc, elp, ne = self._inputs(x0, goal, leg, cir, nc, elp, ne)
+        u0 = np.ascontiguousarray(u0, np.float64).reshape(B, self.n)
+        lu = None if last_u is None else np.ascontiguousarray(last_u, np.float64).reshape(B, 2)
+        out = dict(u=np.zeros((B, self.n)), foot=np.zeros((B, 3)), x_pred=np.zeros((B, self.cfg.N, self.sdim)),
+                   status=np.zeros(B, np.int32), iters=np.zeros(B, np.int32))
+        rc = self._L.alipmpc_solve_batch(self._h, B, _ptr(x0), _ptr(goal), _ptr(leg), _ptr(cir), _ptr(nc), _ptr(elp),
+                                         _ptr(ne), _ptr(u0), _ptr(lu), _ptr(out["u"]), _ptr(out["foot"]),
+                                         _ptr(out["x_pred"]), _ptr(out["status"]), _ptr(out["iters"]), None)
+        self._check(rc, "alipmpc_solve_batch")
+        return out
+
+    def eval(self, x0, goal, leg, cir, nc, elp=None, ne=None, u=None, last_u=None, want_J=True):
+        B, x0, goal, leg, cir, nc, elp, ne = self._inputs(x0, goal, leg, cir, nc, elp, ne)
+        u = np.ascontiguousarray(u, np.float64).reshape(B, self.n)
+        lu = None if last_u is None else np.ascontiguousarray(last_u, np.float64).reshape(B, 2)
+        mm = self.m_max
+        out = dict(f=np.zeros(B), grad=np.zeros((B, self.n)), c=np.zeros((B, mm)),
+                   J=np.zeros((B, mm, self.n)) if want_J else None, cl=np.zeros((B, mm)), cu=np.zeros((B, mm)),
+                   goal_eff=np.zeros((B, 2)), row_active=np.zeros((B, mm), np.int8))
+        rc = self._L.alipmpc_eval_batch(self._h, B, _ptr(x0), _ptr(goal), _ptr(leg), _ptr(cir), _ptr(nc), _ptr(elp),
+                                        _ptr(ne), _ptr(u), _ptr(lu), _ptr(out["f"]), _ptr(out["grad"]),
+                                        _ptr(out["c"]), _ptr(out["J"]), _ptr(out["cl"]), _ptr(out["cu"]),
+                                        _ptr(out["goal_eff"]), _ptr(out["row_active"]), None)
+        self._check(rc, "alipmpc_eval_batch")
+        return out
+
+    # ---------------------------------------------------------------- device (torch) calls
+    def solve_device(self, inp, out, stream=None):
+        """Asynchronous solve on device tensors.  inp/out: dicts of torch CUDA tensors with the shapes of
+        solve(); stream: torch.cuda.Stream (defaults to the current stream)."""
+        import torch
+        st = stream if stream is not None else torch.cuda.current_stream()
+        B = inp["x0"].shape[0]
+        rc = self._L.alipmpc_solve_batch(
+            self._h, B, _ptr(inp["x0"]), _ptr(inp["goal"]), _ptr(inp["leg"]), _ptr(inp["cir"]), _ptr(inp["nc"]),
+            _ptr(inp.get("elp")), _ptr(inp.get("ne")), _ptr(inp["u0"]), _ptr(inp.get("last_u")),
+            _ptr(out["u"]), _ptr(out.get("foot")), _ptr(out.get("x_pred")), _ptr(out.get("status")),
+            _ptr(out.get("iters")), ctypes.c_void_p(st.cuda_stream))
+        self._check(rc, "alipmpc_solve_batch")
+
+    def eval_device(self, inp, out, stream=None):
+        import torch
+        st = stream if stream is not None else torch.cuda.current_stream()
+        B = inp["x0"].shape[0]
+        rc = self._L.alipmpc_eval_batch(
+            self._h, B, _ptr(inp["x0"]), _ptr(inp["goal"]), _ptr(inp["leg"]), _ptr(inp["cir"]), _ptr(inp["nc"]),
+            _ptr(inp.get("elp")), _ptr(inp.get("ne")), _ptr(inp["u"]), _ptr(inp.get("last_u")),
+            _ptr(out.get("f")), _ptr(out.get("grad")), _ptr(out.get("c")), _ptr(out.get("J")), _ptr(out.get("cl")),
+            _ptr(out.get("cu")), _ptr(out.get("goal_eff")), _ptr(out.get("row_active")),
+            ctypes.c_void_p(st.cuda_stream))
+        self._check(rc, "alipmpc_eval_batch")

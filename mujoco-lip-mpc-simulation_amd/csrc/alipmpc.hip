@@ -1,0 +1,1717 @@
+// alipmpc.hip — MI355X (gfx950) batched ALIP-MPC-CBF footstep planner: HIP kernels + the C ABI of
+// include/alipmpc.h.
+//
+// What it replaces (reference /root/reference):
+//   MPCCBF.select_obs / solveMPCCBF / gen_control_test rollout   MPC_LIP_modi.py:90-112, 197-301, 325-338
+//   LIP_Prob.objective / gradient / constraints / jacobian       MPC_LIP_modi.py:430-583 (+ helpers 586-655)
+//   sig_step variants                                            MPC_LIP_sig_step.py:184-278, 372-496
+//   cyipopt.Problem(...).solve(u0)  (IPOPT + MA57)               MPC_LIP_modi.py:274-296
+//
+// Design (DESIGN.md has the full story):
+//   * one NLP instance per 64-lane wavefront, 4 instances per 256-thread workgroup; every
+//     synchronisation after the prologue is wave-local, so waves finish independently.
+//   * "generator space": the ALIP step-to-step map is affine, so every quantity the NLP touches —
+//     the states x_1..x_N and footholds p_0..p_{N-1} — is V = E x0 + G u with a CONSTANT generator
+//     matrix G (NG = 8(N+1) rows: block k = [x_k(5), p_k(3)]).  G lives in LDS, shared by the block.
+//     Each Jacobian row is <= 4 coefficients on rows of G; each Hessian term is an 8x8 block of one
+//     generator block.  Line-search trial points are V + alpha dV: no re-rollout.
+//   * KKT matrix K = J^T Sigma J + G^T S G  (n x n, n = 5N <= 30) accumulated with
+//     v_mfma_f64_16x16x4_f64 — the A and B fragments of both products are the SAME (row, column)
+//     element, so each lane builds its fragment in registers, no LDS staging of J.
+//   * K -> LDS transpose -> row-per-lane registers -> Cholesky with readlane broadcasts (compile-time
+//     register indices, template on N), forward/back substitution, IPOPT-style inertia correction.
+//   * primal-dual interior point, IPOPT's monotone barrier update, fraction-to-boundary rule and filter
+//     line search; same algorithm and constants as oracle/np_oracle.py and oracle/alipmpc_oracle.c.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/alipmpc.h"
+
+namespace alip {
+
+constexpr int WAVE = 64;
+constexpr int WAVES_PER_BLOCK = 4;
+constexpr int MAX_ROWS = 128;        // padded constraint rows per instance (2 per lane)
+constexpr int FILTER_CAP = 128;      // 2 filter entries per lane
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------------------------------------------------------
+// kernel parameters (by value)
+// ------------------------------------------------------------------------------------------------
+struct KP {
+    int nc_max, ne_max, rps, m_max, mr4, modi, max_iter, select_obs, detour;
+    double tol, acc_tol, q, p, r, gm1, s, detect_r2, leg2, bvx_lo, bvx_hi, bvy_lo, bvy_hi, dth, mu_init;
+    const double* G;   // NG x NCP
+    const double* E;   // NG x 5
+    long long B;
+    const double* x0;
+    const double* goal;
+    const int8_t* leg;
+    const double* cir;
+    const int32_t* nc;
+    const double* elp;
+    const int32_t* ne;
+    const double* u0;
+    // solve outputs
+    double* u_out;
+    double* foot_out;
+    double* x_pred;
+    int32_t* status;
+    int32_t* iters;
+    // eval outputs
+    double* f_out;
+    double* grad_out;
+    double* c_out;
+    double* J_out;
+    double* cl_out;
+    double* cu_out;
+    double* goal_eff_out;
+    int8_t* active_out;
+};
+
+constexpr int KP_DOUBLES = (int)((sizeof(KP) + 15) / 16 * 2);
+
+enum RowType { R_VBX = 0, R_VBY, R_CIR, R_ELP, R_LEG, R_DTH, R_FEN, R_NONE };
+
+template <int N>
+struct Dim {
+    static constexpr int n = 5 * N;
+    static constexpr int NT = (n + 15) / 16;
+    static constexpr int NCP = 16 * NT;
+    static constexpr int NG = 8 * (N + 1);
+    static constexpr int KLD = NCP + 1;
+};
+
+// ------------------------------------------------------------------------------------------------
+// wave-level helpers
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ int lane_id() { return threadIdx.x & (WAVE - 1); }
+
+__device__ __forceinline__ void wave_sync()
+{
+    // LDS hand-off between lanes of ONE wave: drain this wave's LDS ops and stop the compiler from
+    // moving accesses across.  (No s_barrier: the 4 waves of a block run different instances.)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+__device__ __forceinline__ double bcast(double v, int src)
+{
+    int lo = __builtin_amdgcn_readlane(__double2loint(v), src);
+    int hi = __builtin_amdgcn_readlane(__double2hiint(v), src);
+    return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ double wsum(double v)
+{
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+__device__ __forceinline__ void wsum2(double& a, double& b)
+{
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        double ta = __shfl_xor(a, o);
+        double tb = __shfl_xor(b, o);
+        a += ta;
+        b += tb;
+    }
+}
+__device__ __forceinline__ double wmax(double v)
+{
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ double wmin(double v)
+{
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = fmin(v, __shfl_xor(v, o));
+    return v;
+}
+// sum over the 4 lane groups (lanes c, c+16, c+32, c+48)
+__device__ __forceinline__ double gsum(double v)
+{
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    return v;
+}
+
+// ------------------------------------------------------------------------------------------------
+// per-wave LDS workspace
+// ------------------------------------------------------------------------------------------------
+template <int N>
+struct WS {
+    double* V;      // NG  current generator values
+    double* Vt;     // NG  trial values
+    double* dV;     // NG  step
+    double* gfg;    // NG  d f / d V
+    double* CT;     // N+1 cos(theta_k)  (of the V last passed to state_pass)
+    double* ST;     // N+1
+    double* S;      // (N+1) x 64 Hessian blocks
+    double* rcoef;  // mr4 x 4
+    double* ry;     // mr4
+    double* rsig;   // mr4
+    double* rw;     // mr4
+    double* obs;    // circles 3*nc_max, ellipses 5*ne_max, then qa, qb, qc, ek (4*ne_max)
+    double* K;      // NCP x KLD
+    uint8_t* rgen;  // mr4 x 4
+    int* nsel;      // [0] = nc_sel, [1] = ne_sel
+};
+
+// per-wave LDS doubles (16-byte multiple)
+template <int N>
+__host__ __device__ constexpr int ws_doubles(int nc_max, int ne_max, int mr4)
+{
+    int d = 4 * Dim<N>::NG + 2 * (N + 1) + 64 * (N + 1) + 7 * mr4 + 3 * nc_max + 9 * ne_max +
+            Dim<N>::NCP * Dim<N>::KLD + (4 * mr4 + 7) / 8 + 1;
+    return (d + 1) & ~1;
+}
+
+template <int N>
+__device__ WS<N> carve(double* base, int nc_max, int ne_max, int mr4)
+{
+    using D = Dim<N>;
+    WS<N> w;
+    double* p = base;
+    w.V = p; p += D::NG;
+    w.Vt = p; p += D::NG;
+    w.dV = p; p += D::NG;
+    w.gfg = p; p += D::NG;
+    w.CT = p; p += N + 1;
+    w.ST = p; p += N + 1;
+    w.S = p; p += 64 * (N + 1);
+    w.rcoef = p; p += 4 * mr4;
+    w.ry = p; p += mr4;
+    w.rsig = p; p += mr4;
+    w.rw = p; p += mr4;
+    w.obs = p; p += 3 * nc_max + 9 * ne_max;
+    w.K = p; p += D::NCP * D::KLD;
+    w.nsel = reinterpret_cast<int*>(p); p += 1;
+    w.rgen = reinterpret_cast<uint8_t*>(p);
+    return w;
+}
+
+// generator row indices
+__device__ __forceinline__ int gx(int k, int c) { return 8 * k + c; }       // state x_k comp c
+__device__ __forceinline__ int gp(int k, int c) { return 8 * k + 5 + c; }   // foothold p_k comp c
+
+// ------------------------------------------------------------------------------------------------
+// row decode + evaluation.  Returns the row type; c = value; coef/gen = Jacobian in generator form.
+// ------------------------------------------------------------------------------------------------
+struct RowInfo {
+    int type, k, slot;
+};
+
+__device__ __forceinline__ RowInfo decode_row(const KP& P, int r, int nc_sel, int ne_sel)
+{
+    RowInfo ri;
+    ri.k = r / P.rps;
+    int l = r - ri.k * P.rps;
+    ri.slot = 0;
+    if (r >= P.m_max) {
+        ri.type = R_NONE;
+    } else if (l == 0) {
+        ri.type = R_VBX;
+    } else if (l == 1) {
+        ri.type = R_VBY;
+    } else if (l < 2 + P.nc_max) {
+        ri.slot = l - 2;
+        ri.type = ri.slot < nc_sel ? R_CIR : R_NONE;
+    } else if (l < 2 + P.nc_max + P.ne_max) {
+        ri.slot = l - 2 - P.nc_max;
+        ri.type = ri.slot < ne_sel ? R_ELP : R_NONE;
+    } else if (l == 2 + P.nc_max + P.ne_max) {
+        ri.type = R_LEG;
+    } else if (l == 3 + P.nc_max + P.ne_max) {
+        ri.type = R_DTH;
+    } else {
+        ri.type = R_FEN;
+    }
+    return ri;
+}
+
+__device__ __forceinline__ void row_bounds(const KP& P, const RowInfo& ri, int leg, double& cl, double& cu)
+{
+    switch (ri.type) {
+    case R_VBX:
+    case R_FEN:
+        cl = P.bvx_lo;
+        cu = P.bvx_hi;
+        break;
+    case R_VBY: {
+        bool pos = (leg > 0) == ((ri.k & 1) == 0);
+        cl = pos ? P.bvy_lo : -P.bvy_hi;
+        cu = pos ? P.bvy_hi : -P.bvy_lo;
+        break;
+    }
+    case R_CIR:
+    case R_ELP:
+        cl = 0.0;
+        cu = INFINITY;
+        break;
+    case R_LEG:
+        cl = 0.0;
+        cu = P.leg2;
+        break;
+    case R_DTH:
+        cl = -P.dth;
+        cu = P.dth;
+        break;
+    default:
+        cl = -INFINITY;
+        cu = INFINITY;
+    }
+}
+
+__device__ __forceinline__ void sabs(double x, double eps, double& v, double& d1, double& d2)
+{
+    if (eps == 0.0) {
+        v = fabs(x);
+        d1 = x == 0.0 ? 0.0 : copysign(1.0, x);
+        d2 = 0.0;
+    } else {
+        double r = sqrt(x * x + eps * eps);
+        v = r;
+        d1 = x / r;
+        d2 = eps * eps / (r * r * r);
+    }
+}
+
+template <int N, bool JAC>
+__device__ double row_eval(const KP& P, const RowInfo& ri, const double* V, const double* CT, const double* ST,
+                           const double* obs, double eps, double* coef, int* gen)
+{
+    const int k = ri.k;
+    double c = 0.0;
+    if (JAC) {
+        coef[0] = coef[1] = coef[2] = coef[3] = 0.0;
+        gen[0] = gen[1] = gen[2] = gen[3] = 0;
+    }
+    switch (ri.type) {
+    case R_VBX:
+    case R_VBY:
+    case R_FEN: {
+        double ct = CT[k + 1], st = ST[k + 1];
+        double vx = V[gx(k + 1, 2)], vy = V[gx(k + 1, 3)];
+        double vbx = ct * vx + st * vy;
+        if (ri.type == R_VBY) {
+            c = -st * vx + ct * vy;
+            if (JAC) {
+                coef[0] = -st; coef[1] = ct; coef[2] = -ct * vx - st * vy;
+                gen[0] = gx(k + 1, 2); gen[1] = gx(k + 1, 3); gen[2] = gx(k + 1, 4);
+            }
+        } else {
+            c = vbx;
+            if (JAC) {
+                coef[0] = ct; coef[1] = st; coef[2] = -st * vx + ct * vy;
+                gen[0] = gx(k + 1, 2); gen[1] = gx(k + 1, 3); gen[2] = gx(k + 1, 4);
+            }
+            if (ri.type == R_FEN) {
+                double a, d1, d2;
+                sabs(V[gp(k, 2)], eps, a, d1, d2);
+                c += P.s * a;
+                if (JAC) {
+                    coef[3] = P.s * d1;
+                    gen[3] = gp(k, 2);
+                }
+            }
+        }
+        break;
+    }
+    case R_CIR: {
+        const double* o = obs + 3 * ri.slot;
+        double x1 = V[gx(k + 1, 0)] - o[0], y1 = V[gx(k + 1, 1)] - o[1];
+        double x0 = V[gx(k, 0)] - o[0], y0 = V[gx(k, 1)] - o[1];
+        double rr = o[2] * o[2];
+        c = (x1 * x1 + y1 * y1 - rr) + P.gm1 * (x0 * x0 + y0 * y0 - rr);
+        if (JAC) {
+            coef[0] = 2 * x1; coef[1] = 2 * y1; coef[2] = P.gm1 * 2 * x0; coef[3] = P.gm1 * 2 * y0;
+            gen[0] = gx(k + 1, 0); gen[1] = gx(k + 1, 1); gen[2] = gx(k, 0); gen[3] = gx(k, 1);
+        }
+        break;
+    }
+    case R_ELP: {
+        const double* o = obs + 3 * P.nc_max + 5 * ri.slot;
+        const double* qq = obs + 3 * P.nc_max + 5 * P.ne_max;
+        double qa = qq[ri.slot], qb = qq[P.ne_max + ri.slot], qc = qq[2 * P.ne_max + ri.slot], ek = qq[3 * P.ne_max + ri.slot];
+        double x1 = V[gx(k + 1, 0)] - o[0], y1 = V[gx(k + 1, 1)] - o[1];
+        double x0 = V[gx(k, 0)] - o[0], y0 = V[gx(k, 1)] - o[1];
+        c = (qa * x1 * x1 + qb * x1 * y1 + qc * y1 * y1 - ek) + P.gm1 * (qa * x0 * x0 + qb * x0 * y0 + qc * y0 * y0 - ek);
+        if (JAC) {
+            coef[0] = 2 * qa * x1 + qb * y1; coef[1] = 2 * qc * y1 + qb * x1;
+            coef[2] = P.gm1 * (2 * qa * x0 + qb * y0); coef[3] = P.gm1 * (2 * qc * y0 + qb * x0);
+            gen[0] = gx(k + 1, 0); gen[1] = gx(k + 1, 1); gen[2] = gx(k, 0); gen[3] = gx(k, 1);
+        }
+        break;
+    }
+    case R_LEG: {
+        double ex = V[gx(k, 0)] - V[gp(k, 0)], ey = V[gx(k, 1)] - V[gp(k, 1)];
+        c = ex * ex + ey * ey;
+        if (JAC) {
+            coef[0] = 2 * ex; coef[1] = 2 * ey; coef[2] = -2 * ex; coef[3] = -2 * ey;
+            gen[0] = gx(k, 0); gen[1] = gx(k, 1); gen[2] = gp(k, 0); gen[3] = gp(k, 1);
+        }
+        break;
+    }
+    case R_DTH:
+        c = V[gp(k, 2)];
+        if (JAC) {
+            coef[0] = 1.0;
+            gen[0] = gp(k, 2);
+        }
+        break;
+    default:
+        break;
+    }
+    return c;
+}
+
+// ------------------------------------------------------------------------------------------------
+// state pass: lanes 1..N own state x_k.  Writes CT/ST for the given V; returns this lane's cost term
+// (0 elsewhere).  If GRAD, writes d f / d V into gfg (all NG entries).
+// ------------------------------------------------------------------------------------------------
+template <int N, bool GRAD>
+__device__ double state_pass(const KP& P, const double* V, double* CT, double* ST, double* gfg, double gxg, double gyg)
+{
+    const int lane = lane_id();
+    double fk = 0.0;
+    if (GRAD) {
+        for (int t = lane; t < Dim<N>::NG; t += WAVE) gfg[t] = 0.0;
+        wave_sync();
+    }
+    if (lane >= 1 && lane <= N) {
+        const int k = lane;
+        double th = V[gx(k, 4)];
+        double s_, c_;
+        sincos(th, &s_, &c_);
+        CT[k] = c_;
+        ST[k] = s_;
+        double px = V[gx(k, 0)], py = V[gx(k, 1)];
+        double w = P.q + (k == 1 ? P.p : 0.0);
+        double ex = px - gxg, ey = py - gyg;
+        double dxg = gxg - px, dyg = gyg - py;
+        double phi = th - atan2(dyg, dxg);
+        fk = w * (ex * ex + ey * ey) + P.r * phi * phi;
+        if (GRAD) {
+            double rho2 = dxg * dxg + dyg * dyg;
+            gfg[gx(k, 0)] = 2 * w * ex + 2 * P.r * phi * (-dyg / rho2);
+            gfg[gx(k, 1)] = 2 * w * ey + 2 * P.r * phi * (dxg / rho2);
+            gfg[gx(k, 4)] = 2 * P.r * phi;
+        }
+    }
+    return fk;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Hessian blocks: lane kb (0..N) writes S block kb (8x8, symmetric) of L = f - y^T c
+// ------------------------------------------------------------------------------------------------
+template <int N>
+__device__ void hess_pass(const KP& P, const WS<N>& w, double eps, double gxg, double gyg)
+{
+    const int lane = lane_id();
+    if (lane > N) return;
+    const int kb = lane;
+    double* S = w.S + 64 * kb;
+    const double* V = w.V;
+    const int nc_sel = w.nsel[0], ne_sel = w.nsel[1];
+    double h00 = 0, h01 = 0, h11 = 0, h04 = 0, h14 = 0, h44 = 0, h24 = 0, h34 = 0;
+    double h05 = 0, h55 = 0, h77 = 0;
+    const double* qq = w.obs + 3 * P.nc_max + 5 * P.ne_max;
+    if (kb >= 1) {
+        double px = V[gx(kb, 0)], py = V[gx(kb, 1)], th = V[gx(kb, 4)];
+        double wq = P.q + (kb == 1 ? P.p : 0.0);
+        double dxg = gxg - px, dyg = gyg - py;
+        double rho2 = dxg * dxg + dyg * dyg, r4 = rho2 * rho2;
+        double phi = th - atan2(dyg, dxg);
+        double gp0 = -dyg / rho2, gp1 = dxg / rho2;
+        double s00 = 2 * dxg * dyg / r4, s01 = (dyg * dyg - dxg * dxg) / r4, s11 = -2 * dxg * dyg / r4;
+        h00 = 2 * wq + 2 * P.r * (gp0 * gp0 - phi * s00);
+        h01 = 2 * P.r * (gp0 * gp1 - phi * s01);
+        h11 = 2 * wq + 2 * P.r * (gp1 * gp1 - phi * s11);
+        h04 = 2 * P.r * gp0;
+        h14 = 2 * P.r * gp1;
+        h44 = 2 * P.r;
+        // rows of step kb-1 act on x_kb as the post-step state
+        const int base = (kb - 1) * P.rps;
+        double ct = w.CT[kb], st = w.ST[kb];
+        double vx = V[gx(kb, 2)], vy = V[gx(kb, 3)];
+        double vbx = ct * vx + st * vy, vby = -st * vx + ct * vy;
+        double wbx = w.ry[base + 0] + (P.modi ? w.ry[base + P.rps - 1] : 0.0);
+        double wby = w.ry[base + 1];
+        h24 = wbx * st + wby * ct;
+        h34 = -wbx * ct + wby * st;
+        h44 += wbx * vbx + wby * vby;
+        for (int j = 0; j < nc_sel; ++j) {
+            double y = w.ry[base + 2 + j];
+            h00 -= 2 * y;
+            h11 -= 2 * y;
+        }
+        for (int j = 0; j < ne_sel; ++j) {
+            double y = w.ry[base + 2 + P.nc_max + j];
+            h00 -= y * 2 * qq[j];
+            h01 -= y * qq[P.ne_max + j];
+            h11 -= y * 2 * qq[2 * P.ne_max + j];
+        }
+    }
+    if (kb < N) {
+        const int base = kb * P.rps;
+        if (kb >= 1) {
+            for (int j = 0; j < nc_sel; ++j) {
+                double y = w.ry[base + 2 + j] * P.gm1;
+                h00 -= 2 * y;
+                h11 -= 2 * y;
+            }
+            for (int j = 0; j < ne_sel; ++j) {
+                double y = w.ry[base + 2 + P.nc_max + j] * P.gm1;
+                h00 -= y * 2 * qq[j];
+                h01 -= y * qq[P.ne_max + j];
+                h11 -= y * 2 * qq[2 * P.ne_max + j];
+            }
+        }
+        double yl = w.ry[base + 2 + P.nc_max + P.ne_max];
+        h00 -= 2 * yl;
+        h11 -= 2 * yl;
+        h05 = 2 * yl;
+        h55 = -2 * yl;
+        if (P.modi && eps != 0.0) {
+            double a, d1, d2;
+            sabs(V[gp(kb, 2)], eps, a, d1, d2);
+            h77 = -w.ry[base + P.rps - 1] * P.s * d2;
+        }
+    }
+    S[0 * 8 + 0] = h00; S[0 * 8 + 1] = h01; S[1 * 8 + 0] = h01; S[1 * 8 + 1] = h11;
+    S[0 * 8 + 4] = h04; S[4 * 8 + 0] = h04; S[1 * 8 + 4] = h14; S[4 * 8 + 1] = h14;
+    S[2 * 8 + 4] = h24; S[4 * 8 + 2] = h24; S[3 * 8 + 4] = h34; S[4 * 8 + 3] = h34; S[4 * 8 + 4] = h44;
+    S[0 * 8 + 5] = h05; S[5 * 8 + 0] = h05; S[1 * 8 + 6] = h05; S[6 * 8 + 1] = h05;
+    S[5 * 8 + 5] = h55; S[6 * 8 + 6] = h55; S[7 * 8 + 7] = h77;
+}
+
+// J[r][col] from the generator form
+__device__ __forceinline__ double jrow_col(const double* rcoef, const uint8_t* rgen, const double* G, int ldg, int r,
+                                           int col)
+{
+    const double* cf = rcoef + 4 * r;
+    const uint8_t* gn = rgen + 4 * r;
+    return cf[0] * G[gn[0] * ldg + col] + cf[1] * G[gn[1] * ldg + col] + cf[2] * G[gn[2] * ldg + col] +
+           cf[3] * G[gn[3] * ldg + col];
+}
+
+// ------------------------------------------------------------------------------------------------
+// instance prologue: load inputs, select_obs, detour goal, ellipse forms, V = E x0 + G u0
+// ------------------------------------------------------------------------------------------------
+template <int N>
+__device__ void prologue(const KP& P, const WS<N>& w, const double* G, const double* E, long long b, double& gxg,
+                         double& gyg, int& legv, double& uj)
+{
+    using D = Dim<N>;
+    const int lane = lane_id();
+    const double* x0 = P.x0 + 5 * b;
+    legv = P.leg[b];
+    const int ncr = P.nc[b];
+    const int ner = P.ne ? P.ne[b] : 0;
+    double x0v0 = x0[0], x0v1 = x0[1];
+    double g0 = P.goal[2 * b], g1 = P.goal[2 * b + 1];
+    // select_obs (MPC_LIP_modi.py:325-338): keep order, compact into the first slots
+    {
+        bool valid = lane < ncr && lane < P.nc_max;
+        double c0 = 0, c1 = 0, c2 = 0;
+        if (valid) {
+            const double* c = P.cir + ((size_t)b * P.nc_max + lane) * 3;
+            c0 = c[0]; c1 = c[1]; c2 = c[2];
+        }
+        double d = (x0v0 - c0) * (x0v0 - c0) + (x0v1 - c1) * (x0v1 - c1) - c2 * c2;
+        bool keep = valid && (!P.select_obs || d <= P.detect_r2);
+        unsigned long long m = __ballot(keep);
+        int pos = __builtin_popcountll(m & ((1ull << lane) - 1ull));
+        if (keep) {
+            w.obs[3 * pos + 0] = c0;
+            w.obs[3 * pos + 1] = c1;
+            w.obs[3 * pos + 2] = c2;
+        }
+        if (lane == 0) w.nsel[0] = __builtin_popcountll(m);
+    }
+    if (P.ne_max > 0) {
+        bool valid = lane < ner && lane < P.ne_max;
+        double e[5] = {0, 0, 0, 0, 0};
+        if (valid) {
+            const double* ep = P.elp + ((size_t)b * P.ne_max + lane) * 5;
+            for (int i = 0; i < 5; ++i) e[i] = ep[i];
+        }
+        double rmax = e[2] > e[3] ? e[2] : e[3];
+        double d = (x0v0 - e[0]) * (x0v0 - e[0]) + (x0v1 - e[1]) * (x0v1 - e[1]) - rmax * rmax;
+        bool keep = valid && (!P.select_obs || d <= P.detect_r2);
+        unsigned long long m = __ballot(keep);
+        int pos = __builtin_popcountll(m & ((1ull << lane) - 1ull));
+        if (keep) {
+            double* o = w.obs + 3 * P.nc_max + 5 * pos;
+            for (int i = 0; i < 5; ++i) o[i] = e[i];
+            double ce, se;
+            sincos(e[4], &se, &ce);
+            double* qq = w.obs + 3 * P.nc_max + 5 * P.ne_max;
+            qq[pos] = (e[3] * ce) * (e[3] * ce) + (e[2] * se) * (e[2] * se);
+            qq[P.ne_max + pos] = 2 * ce * se * (e[3] * e[3] - e[2] * e[2]);
+            qq[2 * P.ne_max + pos] = (e[3] * se) * (e[3] * se) + (e[2] * ce) * (e[2] * ce);
+            qq[3 * P.ne_max + pos] = (e[3] * e[2]) * (e[3] * e[2]);
+        }
+        if (lane == 0) w.nsel[1] = __builtin_popcountll(m);
+    } else if (lane == 0) {
+        w.nsel[1] = 0;
+    }
+    wave_sync();
+    // detour goal (MPC_LIP_modi.py:247-271): first selected circle that triggers
+    gxg = g0;
+    gyg = g1;
+    if (P.detour) {
+        const int ncs = w.nsel[0];
+        bool fire = false;
+        double nx = 0, ny = 0;
+        if (lane < ncs) {
+            const double* c = w.obs + 3 * lane;
+            double cen = (x0v0 - c[0]) * (x0v0 - c[0]) + (x0v1 - c[1]) * (x0v1 - c[1]);
+            double gd = (x0v0 - g0) * (x0v0 - g0) + (x0v1 - g1) * (x0v1 - g1);
+            if (cen < gd && cen < 9 * c[2] * c[2]) {
+                double th = atan2(g1 - x0v1, g0 - x0v0);
+                double al = atan2(c[1] - x0v1, c[0] - x0v0);
+                double dd = th - al;
+                if (dd < 0 && fabs(dd) > M_PI)
+                    dd += 2 * M_PI;
+                else if (dd > 0 && fabs(dd) > M_PI)
+                    dd -= 2 * M_PI;
+                if (fabs(dd) < M_PI / 12) {
+                    fire = true;
+                    double na = dd < 0 ? th - M_PI / 12 : th + M_PI / 12;
+                    double rr = sqrt(gd);
+                    double sn, cs;
+                    sincos(na, &sn, &cs);
+                    nx = x0v0 + rr * cs;
+                    ny = x0v1 + rr * sn;
+                }
+            }
+        }
+        unsigned long long m = __ballot(fire);
+        if (m) {
+            int first = __builtin_ctzll(m);
+            gxg = bcast(nx, first);
+            gyg = bcast(ny, first);
+        }
+    }
+    // V = E x0 + G u0
+    uj = lane < D::n ? P.u0[(size_t)b * D::n + lane] : 0.0;
+    double xv = lane < 5 ? x0[lane] : 0.0;
+    double xb[5];
+#pragma unroll
+    for (int c = 0; c < 5; ++c) xb[c] = bcast(xv, c);
+    if (lane < D::n) w.Vt[lane] = uj;
+    wave_sync();
+    for (int t = lane; t < D::NG; t += WAVE) {
+        double v = 0.0;
+#pragma unroll
+        for (int c = 0; c < 5; ++c) v += E[t * 5 + c] * xb[c];
+        const double* gr = G + t * D::NCP;
+#pragma unroll
+        for (int j = 0; j < D::n; ++j) v += gr[j] * w.Vt[j];
+        w.V[t] = v;
+    }
+    wave_sync();
+}
+
+// ------------------------------------------------------------------------------------------------
+// register Cholesky: lane i (< n) holds row i of the (regularised) KKT matrix in a[0..n-1].
+// Right-looking; column j is broadcast with readlane (uniform lane index, compile-time register).
+// On success lane i holds row i of L in a[0..i] and idg[j] = 1 / L[j][j] (uniform).
+// ------------------------------------------------------------------------------------------------
+template <int n>
+__device__ __forceinline__ bool chol_rows(double (&a)[n], double& myidg, int lane)
+{
+#pragma unroll
+    for (int j = 0; j < n; ++j) {
+        const double d = bcast(a[j], j);
+        if (!(d > 0.0)) return false;   // wave-uniform
+        const double dj = sqrt(d);
+        const double inv = 1.0 / dj;
+        myidg = lane == j ? inv : myidg;
+        const double lij = a[j] * inv;
+        a[j] = lane == j ? dj : lij;
+#pragma unroll
+        for (int k = j + 1; k < n; ++k) a[k] -= lij * bcast(lij, k);
+    }
+    return true;
+}
+
+// ------------------------------------------------------------------------------------------------
+// the solve kernel: one instance per wave
+// ------------------------------------------------------------------------------------------------
+template <int N, int RPL>
+__global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
+{
+    using D = Dim<N>;
+    constexpr int n = D::n;
+    constexpr int NT = D::NT;
+    constexpr int NCP = D::NCP;
+    constexpr int NG = D::NG;
+    constexpr int KLD = D::KLD;
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    // kernel parameters live in LDS: keeps ~90 kernarg SGPRs from being pinned across the solve
+    KP* Ps = reinterpret_cast<KP*>(smem);
+    double* G = smem + KP_DOUBLES;
+    double* E = G + NG * NCP;
+    double* wsb = E + NG * 5 + ((NG * 5) & 1);
+    if (threadIdx.x == 0) *Ps = Pv;
+    for (int i = threadIdx.x; i < NG * NCP; i += blockDim.x) G[i] = Pv.G[i];
+    for (int i = threadIdx.x; i < NG * 5; i += blockDim.x) E[i] = Pv.E[i];
+    __syncthreads();
+    const KP& P = *Ps;
+    const int wv = threadIdx.x / WAVE;
+    const int lane = lane_id();
+    const long long b = (long long)blockIdx.x * WAVES_PER_BLOCK + wv;
+    if (b >= P.B) return;
+    WS<N> w = carve<N>(wsb + (size_t)wv * ws_doubles<N>(P.nc_max, P.ne_max, P.mr4), P.nc_max, P.ne_max, P.mr4);
+    for (int i = lane; i < 64 * (N + 1); i += WAVE) w.S[i] = 0.0;
+
+    double gxg, gyg, uj;
+    int legv;
+    prologue<N>(P, w, G, E, b, gxg, gyg, legv, uj);
+    const int nc_sel = w.nsel[0], ne_sel = w.nsel[1];
+    const int g4 = lane >> 4, col = lane & 15;
+
+    RowInfo ri[RPL];
+    double cl[RPL], cu[RPL], clo[RPL], cuo[RPL], cr[RPL], sr[RPL], zl[RPL], zu[RPL];
+    bool hl[RPL], hu[RPL];
+    double mu = P.mu_init;
+    double eps = P.modi ? 0.1 * sqrt(mu) : 0.0;
+    state_pass<N, false>(P, w.V, w.CT, w.ST, w.gfg, gxg, gyg);
+    wave_sync();
+    double th0 = 0.0, nbl = 0.0, mal = 0.0;
+#pragma unroll
+    for (int q = 0; q < RPL; ++q) {
+        const int r = lane + WAVE * q;
+        ri[q] = decode_row(P, r, nc_sel, ne_sel);
+        row_bounds(P, ri[q], legv, clo[q], cuo[q]);
+        hl[q] = isfinite(clo[q]);
+        hu[q] = isfinite(cuo[q]);
+        nbl += (double)hl[q] + (double)hu[q];
+        mal += ri[q].type != R_NONE ? 1.0 : 0.0;
+        cl[q] = hl[q] ? clo[q] - 1e-8 * fmax(1.0, fabs(clo[q])) : -INFINITY;
+        cu[q] = hu[q] ? cuo[q] + 1e-8 * fmax(1.0, fabs(cuo[q])) : INFINITY;
+        cr[q] = row_eval<N, false>(P, ri[q], w.V, w.CT, w.ST, w.obs, eps, nullptr, nullptr);
+        double v = cr[q];
+        const double pl = hl[q] ? fmin(1e-2 * fmax(1.0, fabs(cl[q])), 1e-2 * (cu[q] - cl[q])) : 0.0;
+        const double pu = hu[q] ? fmin(1e-2 * fmax(1.0, fabs(cu[q])), 1e-2 * (cu[q] - cl[q])) : 0.0;
+        if (hl[q] && hu[q])
+            v = fmin(fmax(v, cl[q] + pl), cu[q] - pu);
+        else if (hl[q])
+            v = fmax(v, cl[q] + pl);
+        else if (hu[q])
+            v = fmin(v, cu[q] - pu);
+        sr[q] = v;
+        zl[q] = hl[q] ? 1.0 : 0.0;
+        zu[q] = hu[q] ? 1.0 : 0.0;
+        th0 += fabs(cr[q] - sr[q]);
+    }
+    wsum2(th0, nbl);
+    const double m_act = wsum(mal);
+    const double theta_max = 1e4 * fmax(1.0, th0), theta_min = 1e-4 * fmax(1.0, th0);
+    double fth[2] = {INFINITY, INFINITY}, fph[2] = {INFINITY, INFINITY};
+    int nf = 0;
+    double dw_last = 0.0;
+    int status = -1, it = 0;
+    double e0 = INFINITY;
+    const double gth = 1e-5, gph = 1e-8, sth = 1.1, sph = 2.3, eta = 1e-8, gal = 0.05;
+
+    for (it = 0; it <= P.max_iter; ++it) {
+        double f = 0.0, gfc[NT], ryc[NT];
+        bool reeval = false;
+        for (;;) {
+            // ---- evaluation at V
+            {
+                const double fk = state_pass<N, true>(P, w.V, w.CT, w.ST, w.gfg, gxg, gyg);
+                f = wsum(fk);
+                wave_sync();
+#pragma unroll
+                for (int q = 0; q < RPL; ++q) {
+                    const int r = lane + WAVE * q;
+                    if (r < P.mr4) {
+                        double cf[4];
+                        int gn[4];
+                        cr[q] = row_eval<N, true>(P, ri[q], w.V, w.CT, w.ST, w.obs, eps, cf, gn);
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            w.rcoef[4 * r + i] = cf[i];
+                            w.rgen[4 * r + i] = (uint8_t)gn[i];
+                        }
+                        w.ry[r] = zl[q] - zu[q];
+                    }
+                }
+                wave_sync();
+            }
+            // ---- grad f and J^T y in the MFMA lane layout (column = lane & 15), reduced over the 4 groups
+#pragma unroll
+            for (int T = 0; T < NT; ++T) {
+                gfc[T] = 0.0;
+                ryc[T] = 0.0;
+            }
+            for (int s4 = 0; s4 < P.mr4; s4 += 4) {
+                const int r = s4 + g4;
+                const double y = w.ry[r];
+#pragma unroll
+                for (int T = 0; T < NT; ++T) ryc[T] += jrow_col(w.rcoef, w.rgen, G, NCP, r, 16 * T + col) * y;
+            }
+            for (int t = 4 + g4; t < NG; t += 4) {
+                const double gv = w.gfg[t];
+#pragma unroll
+                for (int T = 0; T < NT; ++T) gfc[T] += G[t * NCP + 16 * T + col] * gv;
+            }
+#pragma unroll
+            for (int T = 0; T < NT; ++T) {
+                gfc[T] = gsum(gfc[T]);
+                ryc[T] = gsum(ryc[T]);
+            }
+            if (reeval) break;
+            // ---- convergence test (IPOPT scaled overall error) and barrier update
+            double ru = 0.0;
+#pragma unroll
+            for (int T = 0; T < NT; ++T)
+                if (g4 == 0 && 16 * T + col < n) ru = fmax(ru, fabs(gfc[T] - ryc[T]));
+            double rcm = 0.0, nz = 0.0, comp0 = 0.0;
+#pragma unroll
+            for (int q = 0; q < RPL; ++q) {
+                const double dl = hl[q] ? sr[q] - cl[q] : 1.0, du = hu[q] ? cu[q] - sr[q] : 1.0;
+                if (ri[q].type != R_NONE) rcm = fmax(rcm, fabs(cr[q] - sr[q]));
+                nz += fabs(zl[q]) + fabs(zu[q]);
+                if (hl[q]) comp0 = fmax(comp0, fabs(dl * zl[q]));
+                if (hu[q]) comp0 = fmax(comp0, fabs(du * zu[q]));
+            }
+            ru = wmax(ru);
+            rcm = wmax(rcm);
+            nz = wsum(nz);
+            comp0 = wmax(comp0);
+            const double sd = fmax(100.0, nz / (m_act + n)) / 100.0;
+            const double sc = fmax(100.0, nz / fmax(1.0, nbl)) / 100.0;
+            const double base_err = fmax(ru / sd, rcm);
+            e0 = fmax(base_err, comp0 / sc);
+            if (e0 <= P.tol) {
+                status = 0;
+                break;
+            }
+            if (it == P.max_iter) break;
+            const double mu_min = P.tol / 10.0;
+            const double mu_prev = mu;
+            for (int t = 0; t < 8; ++t) {
+                double cm = 0.0;
+#pragma unroll
+                for (int q = 0; q < RPL; ++q) {
+                    const double dl = hl[q] ? sr[q] - cl[q] : 1.0, du = hu[q] ? cu[q] - sr[q] : 1.0;
+                    if (hl[q]) cm = fmax(cm, fabs(dl * zl[q] - mu));
+                    if (hu[q]) cm = fmax(cm, fabs(du * zu[q] - mu));
+                }
+                cm = wmax(cm);
+                if (fmax(base_err, cm / sc) <= 10.0 * mu && mu > mu_min)
+                    mu = fmax(mu_min, fmin(0.2 * mu, pow(mu, 1.5)));
+                else
+                    break;
+            }
+            if (mu != mu_prev) {
+                nf = 0;
+                if (P.modi) {
+                    eps = 0.1 * sqrt(mu);
+                    reeval = true;
+                    continue;
+                }
+            }
+            break;
+        }
+        if (status == 0 || it == P.max_iter) break;
+        const double tau = fmax(0.99, 1.0 - mu);
+
+        // ---- KKT: Sigma, w, Hessian blocks; K = J^T Sigma J + G^T S G by f64 MFMA
+        double rcv[RPL];
+#pragma unroll
+        for (int q = 0; q < RPL; ++q) {
+            const int r = lane + WAVE * q;
+            const double dl = hl[q] ? sr[q] - cl[q] : 1.0, du = hu[q] ? cu[q] - sr[q] : 1.0;
+            const double sg = (hl[q] ? zl[q] / dl : 0.0) + (hu[q] ? zu[q] / du : 0.0);
+            rcv[q] = cr[q] - sr[q];
+            if (r < P.mr4) {
+                w.rsig[r] = sg;
+                w.rw[r] = (hl[q] ? mu / dl : 0.0) - (hu[q] ? mu / du : 0.0) - sg * rcv[q];
+            }
+        }
+        hess_pass<N>(P, w, eps, gxg, gyg);
+        wave_sync();
+        double rhsc[NT];
+        {
+            d4 acc[NT * (NT + 1) / 2];
+#pragma unroll
+            for (int i = 0; i < NT * (NT + 1) / 2; ++i) acc[i] = d4{0.0, 0.0, 0.0, 0.0};
+            double pw[NT];
+#pragma unroll
+            for (int T = 0; T < NT; ++T) pw[T] = 0.0;
+            for (int s4 = 0; s4 < P.mr4; s4 += 4) {
+                const int r = s4 + g4;
+                const double sg = w.rsig[r], wr = w.rw[r];
+                double jv[NT];
+#pragma unroll
+                for (int T = 0; T < NT; ++T) {
+                    jv[T] = jrow_col(w.rcoef, w.rgen, G, NCP, r, 16 * T + col);
+                    pw[T] += jv[T] * wr;
+                }
+                acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(jv[0], sg * jv[0], acc[0], 0, 0, 0);
+                if constexpr (NT == 2) {
+                    acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(jv[0], sg * jv[1], acc[1], 0, 0, 0);
+                    acc[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(jv[1], sg * jv[1], acc[2], 0, 0, 0);
+                }
+            }
+            for (int t0 = 4; t0 < NG; t0 += 4) {
+                const int t = t0 + g4;
+                const int kb = t >> 3, c = t & 7;
+                const double* Srow = w.S + 64 * kb + 8 * c;
+                const double* Gb = G + 8 * kb * NCP;
+                double gv[NT], sgv[NT];
+#pragma unroll
+                for (int T = 0; T < NT; ++T) {
+                    gv[T] = G[t * NCP + 16 * T + col];
+                    double a = 0.0;
+#pragma unroll
+                    for (int c2 = 0; c2 < 8; ++c2) a += Srow[c2] * Gb[c2 * NCP + 16 * T + col];
+                    sgv[T] = a;
+                }
+                acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(gv[0], sgv[0], acc[0], 0, 0, 0);
+                if constexpr (NT == 2) {
+                    acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(gv[0], sgv[1], acc[1], 0, 0, 0);
+                    acc[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(gv[1], sgv[1], acc[2], 0, 0, 0);
+                }
+            }
+#pragma unroll
+            for (int T = 0; T < NT; ++T) rhsc[T] = gsum(pw[T]) - gfc[T];
+            // C/D layout of v_mfma_f64_16x16x4: lane holds D[g4 + 4*i][col], i = 0..3
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int row = g4 + 4 * i;
+                w.K[row * KLD + col] = acc[0][i];
+                if constexpr (NT == 2) {
+                    w.K[row * KLD + 16 + col] = acc[1][i];
+                    w.K[(16 + col) * KLD + row] = acc[1][i];
+                    w.K[(16 + row) * KLD + 16 + col] = acc[2][i];
+                }
+            }
+        }
+        wave_sync();
+        // ---- factor with inertia correction, solve for du
+        double xv;
+        {
+            double rhs_l = 0.0;
+#pragma unroll
+            for (int T = 0; T < NT; ++T) rhs_l = (lane < n && (lane >> 4) == T) ? rhsc[T] : rhs_l;
+            double a[n];
+            double myidg = 1.0;
+#pragma unroll
+            for (int j = 0; j < n; ++j) a[j] = lane < n ? w.K[lane * KLD + j] : (lane == j ? 1.0 : 0.0);
+            if (!chol_rows<n>(a, myidg, lane)) {
+                double dw = dw_last == 0.0 ? 1e-4 : fmax(1e-20, dw_last / 3.0);
+                for (;;) {
+#pragma unroll
+                    for (int j = 0; j < n; ++j)
+                        a[j] = (lane < n ? w.K[lane * KLD + j] : (lane == j ? 1.0 : 0.0)) + (lane == j ? dw : 0.0);
+                    if (chol_rows<n>(a, myidg, lane)) break;
+                    dw *= dw_last == 0.0 ? 100.0 : 8.0;
+                    if (dw > 1e40) break;
+                }
+                dw_last = dw;
+            }
+            // forward: L y = rhs
+            double acc = 0.0, yv = 0.0;
+#pragma unroll
+            for (int k = 0; k < n; ++k) {
+                const double yk = bcast((rhs_l - acc) * myidg, k);
+                yv = lane == k ? yk : yv;
+                acc += lane > k ? a[k] * yk : 0.0;
+            }
+            // transpose L through LDS for the backward sweep
+            wave_sync();
+            if (lane < n) {
+#pragma unroll
+                for (int j = 0; j < n; ++j) w.K[lane * KLD + j] = j <= lane ? a[j] : 0.0;
+            }
+            wave_sync();
+            acc = 0.0;
+            xv = 0.0;
+#pragma unroll
+            for (int i = n - 1; i >= 0; --i) {
+                const double xi = bcast((yv - acc) * myidg, i);
+                xv = lane == i ? xi : xv;
+                acc += lane < i ? w.K[i * KLD + (lane & 31)] * xi : 0.0;
+            }
+        }
+        // ---- dV = G du  (du staged through LDS, read as broadcasts)
+        if (lane < n) w.Vt[lane] = xv;
+        wave_sync();
+        for (int t = lane; t < NG; t += WAVE) {
+            const double* gr = G + t * NCP;
+            double v = 0.0;
+#pragma unroll
+            for (int j = 0; j < n; ++j) v += gr[j] * w.Vt[j];
+            w.dV[t] = v;
+        }
+        wave_sync();
+        // ---- slack / multiplier steps, fraction to boundary
+        double dS[RPL], dZl[RPL], dZu[RPL];
+        double ap = 1.0, az = 1.0, theta = 0.0, lsum = 0.0, sl = 0.0;
+#pragma unroll
+        for (int q = 0; q < RPL; ++q) {
+            const int r = lane + WAVE * q;
+            const double dl = hl[q] ? sr[q] - cl[q] : 1.0, du = hu[q] ? cu[q] - sr[q] : 1.0;
+            double jd = 0.0;
+            if (r < P.mr4) {
+                const double* cf = w.rcoef + 4 * r;
+                const uint8_t* gn = w.rgen + 4 * r;
+                jd = cf[0] * w.dV[gn[0]] + cf[1] * w.dV[gn[1]] + cf[2] * w.dV[gn[2]] + cf[3] * w.dV[gn[3]];
+            }
+            dS[q] = jd + rcv[q];
+            dZl[q] = hl[q] ? mu / dl - zl[q] - zl[q] / dl * dS[q] : 0.0;
+            dZu[q] = hu[q] ? mu / du - zu[q] + zu[q] / du * dS[q] : 0.0;
+            if (hl[q] && dS[q] < 0) ap = fmin(ap, -tau * dl / dS[q]);
+            if (hu[q] && dS[q] > 0) ap = fmin(ap, tau * du / dS[q]);
+            if (hl[q] && dZl[q] < 0) az = fmin(az, -tau * zl[q] / dZl[q]);
+            if (hu[q] && dZu[q] < 0) az = fmin(az, -tau * zu[q] / dZu[q]);
+            if (ri[q].type != R_NONE) theta += fabs(rcv[q]);
+            if (hl[q]) {
+                lsum += log(dl);
+                sl += dS[q] / dl;
+            }
+            if (hu[q]) {
+                lsum += log(du);
+                sl -= dS[q] / du;
+            }
+        }
+        double gdv = lane < NG ? w.gfg[lane] * w.dV[lane] : 0.0;
+        ap = wmin(ap);
+        az = wmin(az);
+        wsum2(theta, lsum);
+        wsum2(sl, gdv);
+        const double phi = f - mu * lsum;
+        const double gphi = gdv - mu * sl;
+        double amin;
+        if (gphi < 0) {
+            amin = fmin(gth, gph * theta / -gphi);
+            if (theta <= theta_min) amin = fmin(amin, pow(theta, sth) / pow(-gphi, sph));
+        } else {
+            amin = gth;
+        }
+        amin *= gal;
+        // ---- filter line search on trial points V + a dV
+        double a = ap;
+        bool accepted = false, ftype = false;
+        double ctr[RPL];
+        while (a >= amin) {
+            for (int t = lane; t < NG; t += WAVE) w.Vt[t] = w.V[t] + a * w.dV[t];
+            wave_sync();
+            double fk = state_pass<N, false>(P, w.Vt, w.CT, w.ST, w.gfg, gxg, gyg);
+            wave_sync();
+            double tht = 0.0, lg = 0.0;
+            bool bad = false;
+#pragma unroll
+            for (int q = 0; q < RPL; ++q) {
+                ctr[q] = row_eval<N, false>(P, ri[q], w.Vt, w.CT, w.ST, w.obs, eps, nullptr, nullptr);
+                const double st = sr[q] + a * dS[q];
+                if (ri[q].type != R_NONE) tht += fabs(ctr[q] - st);
+                if (hl[q]) {
+                    const double d = st - cl[q];
+                    if (!(d > 0)) bad = true;
+                    lg += log(d);
+                }
+                if (hu[q]) {
+                    const double d = cu[q] - st;
+                    if (!(d > 0)) bad = true;
+                    lg += log(d);
+                }
+            }
+            double ft = fk;
+            wsum2(ft, tht);
+            lg = wsum(lg);
+            const bool anybad = __ballot(bad) != 0ull;
+            const double pht = anybad ? INFINITY : ft - mu * lg;
+            bool ok = isfinite(pht) && tht < theta_max;
+            if (ok) {
+                const bool b0 = lane < nf && !(tht < fth[0] || pht < fph[0]);
+                const bool b1 = lane + WAVE < nf && !(tht < fth[1] || pht < fph[1]);
+                ok = __ballot(b0 || b1) == 0ull;
+            }
+            if (ok) {
+                const bool switching = gphi < 0 && a * pow(-gphi, sph) > pow(theta, sth);
+                if (switching && theta <= theta_min) {
+                    if (pht <= phi + eta * a * gphi) {
+                        accepted = true;
+                        ftype = true;
+                    }
+                } else if (tht <= (1 - gth) * theta || pht <= phi - gph * theta) {
+                    accepted = true;
+                    ftype = false;
+                }
+            }
+            if (accepted) break;
+            a *= 0.5;
+        }
+        if (accepted) {
+            if (!ftype && nf < FILTER_CAP) {
+                const double vt = (1 - gth) * theta, vp = phi - gph * theta;
+                if ((nf & (WAVE - 1)) == lane) {
+                    fth[nf >> 6] = vt;
+                    fph[nf >> 6] = vp;
+                }
+                nf++;
+            }
+            for (int t = lane; t < NG; t += WAVE) w.V[t] = w.Vt[t];
+            uj += a * xv;
+#pragma unroll
+            for (int q = 0; q < RPL; ++q) {
+                sr[q] += a * dS[q];
+                cr[q] = ctr[q];
+            }
+        } else {
+            // restoration substitute: shortest tried step, slacks reset onto c(u), filter reset
+            a = fmax(a, amin);
+            for (int t = lane; t < NG; t += WAVE) w.V[t] += a * w.dV[t];
+            uj += a * xv;
+            wave_sync();
+            state_pass<N, false>(P, w.V, w.CT, w.ST, w.gfg, gxg, gyg);
+            wave_sync();
+#pragma unroll
+            for (int q = 0; q < RPL; ++q) {
+                cr[q] = row_eval<N, false>(P, ri[q], w.V, w.CT, w.ST, w.obs, eps, nullptr, nullptr);
+                double v = cr[q];
+                const double pl = hl[q] ? fmin(1e-2 * fmax(1.0, fabs(cl[q])), 1e-2 * (cu[q] - cl[q])) : 0.0;
+                const double pu = hu[q] ? fmin(1e-2 * fmax(1.0, fabs(cu[q])), 1e-2 * (cu[q] - cl[q])) : 0.0;
+                if (hl[q] && hu[q])
+                    v = fmin(fmax(v, cl[q] + pl), cu[q] - pu);
+                else if (hl[q])
+                    v = fmax(v, cl[q] + pl);
+                else if (hu[q])
+                    v = fmin(v, cu[q] - pu);
+                sr[q] = v;
+            }
+            nf = 0;
+        }
+#pragma unroll
+        for (int q = 0; q < RPL; ++q) {
+            zl[q] += az * dZl[q];
+            zu[q] += az * dZu[q];
+            if (hl[q]) {
+                const double d = sr[q] - cl[q];
+                zl[q] = fmin(fmax(zl[q], mu / (1e10 * d)), 1e10 * mu / d);
+            } else {
+                zl[q] = 0.0;
+            }
+            if (hu[q]) {
+                const double d = cu[q] - sr[q];
+                zu[q] = fmin(fmax(zu[q], mu / (1e10 * d)), 1e10 * mu / d);
+            } else {
+                zu[q] = 0.0;
+            }
+        }
+        wave_sync();
+    }
+    // ---- status + outputs (violation measured on the reference's exact |.|)
+    wave_sync();
+    if (status != 0) {
+        state_pass<N, false>(P, w.V, w.CT, w.ST, w.gfg, gxg, gyg);
+        wave_sync();
+        double viol = 0.0;
+#pragma unroll
+        for (int q = 0; q < RPL; ++q) {
+            const double c = row_eval<N, false>(P, ri[q], w.V, w.CT, w.ST, w.obs, 0.0, nullptr, nullptr);
+            if (hl[q]) viol = fmax(viol, clo[q] - c);
+            if (hu[q]) viol = fmax(viol, c - cuo[q]);
+        }
+        viol = wmax(viol);
+        if (e0 <= P.acc_tol)
+            status = 1;
+        else if (viol > 1e-4)
+            status = 2;
+    }
+    if (lane < n) P.u_out[(size_t)b * n + lane] = uj;
+    if (P.foot_out && lane < 3) P.foot_out[3 * b + lane] = w.V[gp(0, lane)];
+    if (P.x_pred && lane < 5 * N) P.x_pred[(size_t)b * 5 * N + lane] = w.V[gx(lane / 5 + 1, lane % 5)];
+    if (lane == 0) {
+        if (P.status) P.status[b] = status;
+        if (P.iters) P.iters[b] = it;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// eval kernel ("Jacobian sweep"): f, grad f, c, J, cl, cu, goal_eff, row_active at given u
+// ------------------------------------------------------------------------------------------------
+template <int N>
+__global__ __launch_bounds__(256, 4) void eval_kernel(KP Pv)
+{
+    using D = Dim<N>;
+    constexpr int n = D::n;
+    constexpr int NT = D::NT;
+    constexpr int NCP = D::NCP;
+    constexpr int NG = D::NG;
+    constexpr int RPL = 2;
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    // kernel parameters live in LDS: keeps ~90 kernarg SGPRs from being pinned across the solve
+    KP* Ps = reinterpret_cast<KP*>(smem);
+    double* G = smem + KP_DOUBLES;
+    double* E = G + NG * NCP;
+    double* wsb = E + NG * 5 + ((NG * 5) & 1);
+    if (threadIdx.x == 0) *Ps = Pv;
+    for (int i = threadIdx.x; i < NG * NCP; i += blockDim.x) G[i] = Pv.G[i];
+    for (int i = threadIdx.x; i < NG * 5; i += blockDim.x) E[i] = Pv.E[i];
+    __syncthreads();
+    const KP& P = *Ps;
+    const int wv = threadIdx.x / WAVE;
+    const int lane = lane_id();
+    const long long b = (long long)blockIdx.x * WAVES_PER_BLOCK + wv;
+    if (b >= P.B) return;
+    WS<N> w = carve<N>(wsb + (size_t)wv * ws_doubles<N>(P.nc_max, P.ne_max, P.mr4), P.nc_max, P.ne_max, P.mr4);
+    double gxg, gyg, uj;
+    int legv;
+    prologue<N>(P, w, G, E, b, gxg, gyg, legv, uj);
+    const int nc_sel = w.nsel[0], ne_sel = w.nsel[1];
+    const double fk = state_pass<N, true>(P, w.V, w.CT, w.ST, w.gfg, gxg, gyg);
+    const double f = wsum(fk);
+    wave_sync();
+    const size_t mm = (size_t)P.m_max;
+#pragma unroll
+    for (int q = 0; q < RPL; ++q) {
+        const int r = lane + WAVE * q;
+        if (r < P.mr4) {
+            const RowInfo ri = decode_row(P, r, nc_sel, ne_sel);
+            double cf[4];
+            int gn[4];
+            const double c = row_eval<N, true>(P, ri, w.V, w.CT, w.ST, w.obs, 0.0, cf, gn);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                w.rcoef[4 * r + i] = cf[i];
+                w.rgen[4 * r + i] = (uint8_t)gn[i];
+            }
+            if (r < P.m_max) {
+                double clv, cuv;
+                row_bounds(P, ri, legv, clv, cuv);
+                if (P.c_out) P.c_out[b * mm + r] = c;
+                if (P.cl_out) P.cl_out[b * mm + r] = clv;
+                if (P.cu_out) P.cu_out[b * mm + r] = cuv;
+                if (P.active_out) P.active_out[b * mm + r] = ri.type != R_NONE;
+            }
+        }
+    }
+    wave_sync();
+    const int g4 = lane >> 4, col = lane & 15;
+    if (P.J_out) {
+        for (int s4 = 0; s4 < P.mr4; s4 += 4) {
+            const int r = s4 + g4;
+            if (r < P.m_max) {
+#pragma unroll
+                for (int T = 0; T < NT; ++T) {
+                    const int j = 16 * T + col;
+                    if (j < n) P.J_out[(b * mm + r) * n + j] = jrow_col(w.rcoef, w.rgen, G, NCP, r, j);
+                }
+            }
+        }
+    }
+    double gfc[NT];
+#pragma unroll
+    for (int T = 0; T < NT; ++T) gfc[T] = 0.0;
+    for (int t = 4 + g4; t < NG; t += 4) {
+        const double gv = w.gfg[t];
+#pragma unroll
+        for (int T = 0; T < NT; ++T) gfc[T] += G[t * NCP + 16 * T + col] * gv;
+    }
+#pragma unroll
+    for (int T = 0; T < NT; ++T) {
+        gfc[T] = gsum(gfc[T]);
+        if (P.grad_out && g4 == 0 && 16 * T + col < n) P.grad_out[b * n + 16 * T + col] = gfc[T];
+    }
+    if (lane == 0) {
+        if (P.f_out) P.f_out[b] = f;
+        if (P.goal_eff_out) {
+            P.goal_eff_out[2 * b] = gxg;
+            P.goal_eff_out[2 * b + 1] = gyg;
+        }
+    }
+}
+
+}  // namespace alip
+
+// ================================================================================================
+// host side: constants, handle, C ABI
+// ================================================================================================
+namespace {
+
+using namespace alip;
+
+struct Handle {
+    alipmpc_cfg cfg;
+    int device = 0;
+    int N = 3, n = 15, NG = 32, NCP = 16, rps = 0, m_max = 0, mr4 = 0;
+    double* dG = nullptr;
+    double* dE = nullptr;
+    // staging for host-pointer calls
+    void* stage = nullptr;
+    size_t stage_bytes = 0;
+    hipStream_t own = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool timed = false;
+    std::string err;
+};
+
+int fail(Handle* h, int code, const std::string& msg)
+{
+    if (h) h->err = msg;
+    return code;
+}
+
+#define HIPCHK(h, x)                                                                            \
+    do {                                                                                         \
+        hipError_t e_ = (x);                                                                     \
+        if (e_ != hipSuccess) return fail(h, ALIPMPC_EHIP, std::string(#x ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+void mm(const double* a, const double* b, double* c, int n1, int n2, int n3)
+{
+    for (int i = 0; i < n1; ++i)
+        for (int j = 0; j < n3; ++j) {
+            double s = 0;
+            for (int k = 0; k < n2; ++k) s += a[i * n2 + k] * b[k * n3 + j];
+            c[i * n3 + j] = s;
+        }
+}
+
+// generator tables: V = E x0 + G u, row 8k+c (c<5): x_k[c]; row 8k+5+c (c<3): p_k[c]
+void build_tables(const alipmpc_cfg& cfg, int NCP, std::vector<double>& G, std::vector<double>& E)
+{
+    const int N = cfg.N, n = 5 * N, NG = 8 * (N + 1);
+    const double b = std::sqrt(cfg.g / cfg.H), T = cfg.dt;
+    const double ch = std::cosh(b * T), sh = std::sinh(b * T);
+    double A[25] = {ch, 0, sh / b, 0, 0, 0, ch, 0, sh / b, 0, sh * b, 0, ch, 0, 0, 0, sh * b, 0, ch, 0, 0, 0, 0, 0, 1};
+    double Bm[15] = {1 - ch, 0, 0, 0, 1 - ch, 0, -sh * b, 0, 0, 0, -sh * b, 0, 0, 0, 1};
+    const double a_ = 5.0, b_ = 1.0;
+    const double Dd = a_ * (ch - 1) * (ch - 1) + b_ * (sh * b) * (sh * b);
+    const double Ch = -a_ * (ch - 1) / Dd, Sh = -b_ * sh * b / Dd;
+    double W[15] = {Ch, 0, Sh, 0, 0, 0, Ch, 0, Sh, 0, 0, 0, 0, 0, 1};
+    double MB[25], BWA[25], MA[25], WA[15];
+    mm(Bm, W, MB, 5, 3, 5);
+    mm(MB, A, BWA, 5, 5, 5);
+    for (int i = 0; i < 25; ++i) MA[i] = A[i] - BWA[i];
+    mm(W, A, WA, 3, 5, 5);
+    std::vector<double> Phi((N + 1) * 5 * n, 0.0), Pk((N + 1) * 25, 0.0);
+    for (int i = 0; i < 5; ++i) Pk[i * 5 + i] = 1.0;   // MA^0
+    for (int k = 1; k <= N; ++k) {
+        mm(MA, &Phi[(k - 1) * 5 * n], &Phi[k * 5 * n], 5, 5, n);
+        for (int i = 0; i < 5; ++i)
+            for (int j = 0; j < 5; ++j) Phi[k * 5 * n + i * n + 5 * (k - 1) + j] += MB[i * 5 + j];
+        mm(MA, &Pk[(k - 1) * 25], &Pk[k * 25], 5, 5, 5);
+    }
+    G.assign(NG * NCP, 0.0);
+    E.assign(NG * 5, 0.0);
+    for (int k = 0; k <= N; ++k) {
+        for (int c = 0; c < 5; ++c) {
+            for (int j = 0; j < n; ++j) G[(8 * k + c) * NCP + j] = Phi[k * 5 * n + c * n + j];
+            for (int j = 0; j < 5; ++j) E[(8 * k + c) * 5 + j] = Pk[k * 25 + c * 5 + j];
+        }
+        if (k < N) {
+            std::vector<double> WAPhi(3 * n), WAPk(15);
+            mm(WA, &Phi[k * 5 * n], WAPhi.data(), 3, 5, n);
+            mm(WA, &Pk[k * 25], WAPk.data(), 3, 5, 5);
+            for (int c = 0; c < 3; ++c) {
+                for (int j = 0; j < n; ++j) G[(8 * k + 5 + c) * NCP + j] = -WAPhi[c * n + j];
+                for (int j = 0; j < 5; ++j) G[(8 * k + 5 + c) * NCP + 5 * k + j] += W[c * 5 + j];
+                for (int j = 0; j < 5; ++j) E[(8 * k + 5 + c) * 5 + j] = -WAPk[c * 5 + j];
+            }
+        }
+    }
+}
+
+size_t smem_bytes(const Handle* h)
+{
+    int wsd = 0;
+    switch (h->N) {
+#define WSCASE(NN) \
+    case NN: wsd = ws_doubles<NN>(h->cfg.nc_max, h->cfg.ne_max, h->mr4); break;
+        WSCASE(1) WSCASE(2) WSCASE(3) WSCASE(4) WSCASE(5) WSCASE(6)
+#undef WSCASE
+    }
+    const int e = h->NG * 5 + ((h->NG * 5) & 1);
+    return sizeof(double) * ((size_t)KP_DOUBLES + (size_t)h->NG * h->NCP + e + (size_t)WAVES_PER_BLOCK * wsd);
+}
+
+KP make_kp(const Handle* h, long long B)
+{
+    const alipmpc_cfg& c = h->cfg;
+    KP P;
+    std::memset(&P, 0, sizeof(P));
+    P.nc_max = c.nc_max;
+    P.ne_max = c.ne_max;
+    P.rps = h->rps;
+    P.m_max = h->m_max;
+    P.mr4 = h->mr4;
+    P.modi = c.variant == ALIPMPC_VARIANT_MODI;
+    P.max_iter = c.max_iter;
+    P.select_obs = c.select_obs;
+    P.detour = c.detour;
+    P.tol = c.tol;
+    P.acc_tol = c.acceptable_tol;
+    P.q = c.q;
+    P.p = c.p;
+    P.r = c.r;
+    P.gm1 = c.gamma - 1.0;
+    P.s = c.s;
+    P.detect_r2 = c.detect_r2;
+    P.leg2 = c.leg2_max;
+    P.bvx_lo = c.bvx_lo;
+    P.bvx_hi = c.bvx_hi;
+    P.bvy_lo = c.bvy_lo;
+    P.bvy_hi = c.bvy_hi;
+    P.dth = c.dtheta_max;
+    P.mu_init = c.mu_init;
+    P.G = h->dG;
+    P.E = h->dE;
+    P.B = B;
+    return P;
+}
+
+template <int N>
+hipError_t launch_t(bool solve, const KP& P, size_t smem, hipStream_t st)
+{
+    const unsigned grid = (unsigned)((P.B + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
+    if (solve) {
+        if (P.mr4 <= WAVE) {
+            (void)hipFuncSetAttribute((const void*)solve_kernel<N, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+            hipLaunchKernelGGL((solve_kernel<N, 1>), dim3(grid), dim3(WAVE * WAVES_PER_BLOCK), smem, st, P);
+        } else {
+            (void)hipFuncSetAttribute((const void*)solve_kernel<N, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+            hipLaunchKernelGGL((solve_kernel<N, 2>), dim3(grid), dim3(WAVE * WAVES_PER_BLOCK), smem, st, P);
+        }
+    } else {
+        (void)hipFuncSetAttribute((const void*)eval_kernel<N>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        hipLaunchKernelGGL(eval_kernel<N>, dim3(grid), dim3(WAVE * WAVES_PER_BLOCK), smem, st, P);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch(const Handle* h, bool solve, const KP& P, hipStream_t st)
+{
+    const size_t smem = smem_bytes(h);
+    switch (h->N) {
+    case 1: return launch_t<1>(solve, P, smem, st);
+    case 2: return launch_t<2>(solve, P, smem, st);
+    case 3: return launch_t<3>(solve, P, smem, st);
+    case 4: return launch_t<4>(solve, P, smem, st);
+    case 5: return launch_t<5>(solve, P, smem, st);
+    case 6: return launch_t<6>(solve, P, smem, st);
+    }
+    return hipErrorInvalidValue;
+}
+
+int ensure_stage(Handle* h, size_t bytes)
+{
+    if (h->stage_bytes >= bytes) return 0;
+    if (h->stage) hipFree(h->stage);
+    h->stage = nullptr;
+    h->stage_bytes = 0;
+    HIPCHK(h, hipMalloc(&h->stage, bytes));
+    h->stage_bytes = bytes;
+    return 0;
+}
+
+struct Carver {
+    char* base;
+    size_t off = 0;
+    template <class T>
+    T* take(size_t count)
+    {
+        off = (off + 255) & ~(size_t)255;
+        T* p = reinterpret_cast<T*>(base + off);
+        off += count * sizeof(T);
+        return p;
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+int alipmpc_default_cfg(int32_t variant, int32_t N, alipmpc_cfg* c)
+{
+    if (!c) return ALIPMPC_EINVAL;
+    std::memset(c, 0, sizeof(*c));
+    c->N = N;
+    c->nc_max = 6;
+    c->ne_max = 6;
+    c->variant = variant;
+    c->max_iter = 100;
+    c->precision = ALIPMPC_PREC_FP64;
+    c->select_obs = 1;
+    c->detour = 1;
+    c->tol = 1e-8;
+    c->acceptable_tol = 1e-6;
+    c->dt = 0.4;
+    c->H = 1.0;
+    c->g = 9.81;
+    c->leg2_max = 0.09;
+    c->bvx_lo = 0.4;
+    c->bvx_hi = 0.8;
+    c->bvy_lo = 0.15;
+    c->bvy_hi = 0.35;
+    c->dtheta_max = M_PI / 16;
+    c->q = 1.0;
+    c->p = 0.0;
+    c->r = 50.0;
+    c->gamma = 0.2;
+    c->s = 0.024 * 180 / M_PI;
+    c->detect_r2 = 16.0;
+    c->dd_t = 2.0;
+    c->mu_init = 0.1;
+    if (variant == ALIPMPC_VARIANT_SIG_STEP) {   // MPC_LIP_sig_step.py:38,340-353
+        c->bvy_hi = 0.30;
+        c->p = 2.0;
+        c->r = 15.0;
+        c->gamma = 0.4;
+        c->s = 0.014 * 180 / M_PI;
+        c->select_obs = 0;
+    } else if (variant == ALIPMPC_VARIANT_DD) {  // MPC_DD_sig_step.py:33-37,323-338
+        c->select_obs = 0;
+        c->detour = 0;
+    } else if (variant != ALIPMPC_VARIANT_MODI) {
+        return ALIPMPC_EINVAL;
+    }
+    return ALIPMPC_OK;
+}
+
+int32_t alipmpc_rows_per_step(const alipmpc_cfg* c)
+{
+    if (!c) return 0;
+    if (c->variant == ALIPMPC_VARIANT_DD) return c->nc_max + c->ne_max + 1;
+    return 4 + c->nc_max + c->ne_max + (c->variant == ALIPMPC_VARIANT_MODI ? 1 : 0);
+}
+
+int32_t alipmpc_num_vars(const alipmpc_cfg* c)
+{
+    if (!c) return 0;
+    return c->variant == ALIPMPC_VARIANT_DD ? 2 * c->N : 5 * c->N;
+}
+
+int alipmpc_create(const alipmpc_cfg* cfg, int device, void** handle)
+{
+    if (!cfg || !handle) return ALIPMPC_EINVAL;
+    *handle = nullptr;
+    if (cfg->N < 1 || cfg->N > ALIPMPC_MAX_N || cfg->nc_max < 0 || cfg->ne_max < 0 ||
+        cfg->nc_max + cfg->ne_max > ALIPMPC_MAX_OBS || cfg->max_iter < 0 || cfg->max_iter > FILTER_CAP - 2)
+        return ALIPMPC_EINVAL;
+    if (cfg->variant == ALIPMPC_VARIANT_DD || cfg->precision != ALIPMPC_PREC_FP64) return ALIPMPC_EUNSUPPORTED;
+    if (cfg->variant != ALIPMPC_VARIANT_MODI && cfg->variant != ALIPMPC_VARIANT_SIG_STEP) return ALIPMPC_EINVAL;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return ALIPMPC_ENODEV;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return ALIPMPC_ENODEV;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return ALIPMPC_ENODEV;
+    Handle* h = new Handle();
+    h->cfg = *cfg;
+    h->device = device;
+    h->N = cfg->N;
+    h->n = 5 * cfg->N;
+    h->NG = 8 * (cfg->N + 1);
+    h->NCP = 16 * ((h->n + 15) / 16);
+    h->rps = alipmpc_rows_per_step(cfg);
+    h->m_max = cfg->N * h->rps;
+    h->mr4 = (h->m_max + 3) & ~3;
+    if (h->mr4 > MAX_ROWS) {
+        delete h;
+        return ALIPMPC_EINVAL;
+    }
+    if (hipSetDevice(device) != hipSuccess) {
+        delete h;
+        return ALIPMPC_ENODEV;
+    }
+    std::vector<double> G, E;
+    build_tables(*cfg, h->NCP, G, E);
+    if (hipMalloc(&h->dG, G.size() * sizeof(double)) != hipSuccess ||
+        hipMalloc(&h->dE, E.size() * sizeof(double)) != hipSuccess ||
+        hipMemcpy(h->dG, G.data(), G.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(h->dE, E.data(), E.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
+        hipStreamCreateWithFlags(&h->own, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess) {
+        alipmpc_destroy(h);
+        return ALIPMPC_EHIP;
+    }
+    if (smem_bytes(h) > 160 * 1024) {
+        alipmpc_destroy(h);
+        return ALIPMPC_EUNSUPPORTED;
+    }
+    *handle = h;
+    return ALIPMPC_OK;
+}
+
+static int run_batch(Handle* h, bool solve, int64_t B, const double* x0, const double* goal, const int8_t* leg,
+                     const double* cir, const int32_t* nc, const double* elp, const int32_t* ne, const double* u0,
+                     double* u_out, double* foot_out, double* x_pred, int32_t* status, int32_t* iters, double* f,
+                     double* grad, double* c, double* J, double* cl, double* cu, double* goal_eff, int8_t* row_active,
+                     void* hip_stream)
+{
+    if (!h) return ALIPMPC_EINVAL;
+    if (B < 0) return fail(h, ALIPMPC_EINVAL, "B < 0");
+    if (B == 0) return ALIPMPC_OK;
+    if (!x0 || !goal || !leg || !nc || !u0 || (h->cfg.nc_max > 0 && !cir) || (h->cfg.ne_max > 0 && (!elp || !ne)))
+        return fail(h, ALIPMPC_EINVAL, "missing input pointer");
+    if (solve && !u_out) return fail(h, ALIPMPC_EINVAL, "u_out is required");
+    HIPCHK(h, hipSetDevice(h->device));
+    const alipmpc_cfg& cf = h->cfg;
+    const int n = h->n, N = h->N;
+    const size_t mm_ = (size_t)h->m_max;
+    KP P = make_kp(h, B);
+    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : h->own;
+    if (hip_stream) {
+        P.x0 = x0; P.goal = goal; P.leg = leg; P.cir = cir; P.nc = nc; P.elp = elp; P.ne = ne; P.u0 = u0;
+        P.u_out = u_out; P.foot_out = foot_out; P.x_pred = x_pred; P.status = status; P.iters = iters;
+        P.f_out = f; P.grad_out = grad; P.c_out = c; P.J_out = J; P.cl_out = cl; P.cu_out = cu;
+        P.goal_eff_out = goal_eff; P.active_out = row_active;
+        HIPCHK(h, hipEventRecord(h->ev0, st));
+        HIPCHK(h, launch(h, solve, P, st));
+        HIPCHK(h, hipEventRecord(h->ev1, st));
+        h->timed = true;
+        return ALIPMPC_OK;
+    }
+    // host pointers: stage through the handle's device workspace
+    const size_t Bz = (size_t)B;
+    size_t need = 0;
+    {
+        Carver cv{nullptr};
+        cv.take<double>(Bz * 5); cv.take<double>(Bz * 2); cv.take<int8_t>(Bz); cv.take<double>(Bz * 3 * cf.nc_max);
+        cv.take<int32_t>(Bz); cv.take<double>(Bz * 5 * cf.ne_max); cv.take<int32_t>(Bz); cv.take<double>(Bz * n);
+        cv.take<double>(Bz * n); cv.take<double>(Bz * 3); cv.take<double>(Bz * 5 * N); cv.take<int32_t>(Bz);
+        cv.take<int32_t>(Bz); cv.take<double>(Bz); cv.take<double>(Bz * n); cv.take<double>(Bz * mm_);
+        cv.take<double>(Bz * mm_ * n); cv.take<double>(Bz * mm_); cv.take<double>(Bz * mm_); cv.take<double>(Bz * 2);
+        cv.take<int8_t>(Bz * mm_);
+        need = cv.off + 256;
+    }
+    if (int e = ensure_stage(h, need)) return e;
+    Carver cv{(char*)h->stage};
+    double* d_x0 = cv.take<double>(Bz * 5);
+    double* d_goal = cv.take<double>(Bz * 2);
+    int8_t* d_leg = cv.take<int8_t>(Bz);
+    double* d_cir = cv.take<double>(Bz * 3 * cf.nc_max);
+    int32_t* d_nc = cv.take<int32_t>(Bz);
+    double* d_elp = cv.take<double>(Bz * 5 * cf.ne_max);
+    int32_t* d_ne = cv.take<int32_t>(Bz);
+    double* d_u0 = cv.take<double>(Bz * n);
+    double* d_u = cv.take<double>(Bz * n);
+    double* d_foot = cv.take<double>(Bz * 3);
+    double* d_xp = cv.take<double>(Bz * 5 * N);
+    int32_t* d_st = cv.take<int32_t>(Bz);
+    int32_t* d_it = cv.take<int32_t>(Bz);
+    double* d_f = cv.take<double>(Bz);
+    double* d_g = cv.take<double>(Bz * n);
+    double* d_c = cv.take<double>(Bz * mm_);
+    double* d_J = cv.take<double>(Bz * mm_ * n);
+    double* d_cl = cv.take<double>(Bz * mm_);
+    double* d_cu = cv.take<double>(Bz * mm_);
+    double* d_ge = cv.take<double>(Bz * 2);
+    int8_t* d_ra = cv.take<int8_t>(Bz * mm_);
+    auto h2d = [&](void* d, const void* s, size_t bytes) { return hipMemcpyAsync(d, s, bytes, hipMemcpyHostToDevice, st); };
+    auto d2h = [&](void* d, const void* s, size_t bytes) { return hipMemcpyAsync(d, s, bytes, hipMemcpyDeviceToHost, st); };
+    HIPCHK(h, h2d(d_x0, x0, Bz * 5 * 8));
+    HIPCHK(h, h2d(d_goal, goal, Bz * 2 * 8));
+    HIPCHK(h, h2d(d_leg, leg, Bz));
+    if (cf.nc_max) HIPCHK(h, h2d(d_cir, cir, Bz * 3 * cf.nc_max * 8));
+    HIPCHK(h, h2d(d_nc, nc, Bz * 4));
+    if (cf.ne_max) {
+        HIPCHK(h, h2d(d_elp, elp, Bz * 5 * cf.ne_max * 8));
+        HIPCHK(h, h2d(d_ne, ne, Bz * 4));
+    }
+    HIPCHK(h, h2d(d_u0, u0, Bz * n * 8));
+    P.x0 = d_x0; P.goal = d_goal; P.leg = d_leg; P.cir = d_cir; P.nc = d_nc;
+    P.elp = cf.ne_max ? d_elp : nullptr; P.ne = cf.ne_max ? d_ne : nullptr; P.u0 = d_u0;
+    if (solve) {
+        P.u_out = d_u; P.foot_out = d_foot; P.x_pred = d_xp; P.status = d_st; P.iters = d_it;
+    } else {
+        P.f_out = d_f; P.grad_out = d_g; P.c_out = d_c; P.J_out = J ? d_J : nullptr; P.cl_out = d_cl; P.cu_out = d_cu;
+        P.goal_eff_out = d_ge; P.active_out = d_ra;
+    }
+    HIPCHK(h, hipEventRecord(h->ev0, st));
+    HIPCHK(h, launch(h, solve, P, st));
+    HIPCHK(h, hipEventRecord(h->ev1, st));
+    h->timed = true;
+    if (solve) {
+        HIPCHK(h, d2h(u_out, d_u, Bz * n * 8));
+        if (foot_out) HIPCHK(h, d2h(foot_out, d_foot, Bz * 3 * 8));
+        if (x_pred) HIPCHK(h, d2h(x_pred, d_xp, Bz * 5 * N * 8));
+        if (status) HIPCHK(h, d2h(status, d_st, Bz * 4));
+        if (iters) HIPCHK(h, d2h(iters, d_it, Bz * 4));
+    } else {
+        if (f) HIPCHK(h, d2h(f, d_f, Bz * 8));
+        if (grad) HIPCHK(h, d2h(grad, d_g, Bz * n * 8));
+        if (c) HIPCHK(h, d2h(c, d_c, Bz * mm_ * 8));
+        if (J) HIPCHK(h, d2h(J, d_J, Bz * mm_ * n * 8));
+        if (cl) HIPCHK(h, d2h(cl, d_cl, Bz * mm_ * 8));
+        if (cu) HIPCHK(h, d2h(cu, d_cu, Bz * mm_ * 8));
+        if (goal_eff) HIPCHK(h, d2h(goal_eff, d_ge, Bz * 2 * 8));
+        if (row_active) HIPCHK(h, d2h(row_active, d_ra, Bz * mm_));
+    }
+    HIPCHK(h, hipStreamSynchronize(st));
+    return ALIPMPC_OK;
+}
+
+int alipmpc_solve_batch(void* handle, int64_t B, const double* x0, const double* goal, const int8_t* leg,
+                        const double* cir, const int32_t* nc, const double* elp, const int32_t* ne, const double* u0,
+                        const double* last_u, double* u_out, double* foot_out, double* x_pred, int32_t* status,
+                        int32_t* iters, void* hip_stream)
+{
+    (void)last_u;
+    return run_batch((Handle*)handle, true, B, x0, goal, leg, cir, nc, elp, ne, u0, u_out, foot_out, x_pred, status,
+                     iters, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, hip_stream);
+}
+
+int alipmpc_eval_batch(void* handle, int64_t B, const double* x0, const double* goal, const int8_t* leg,
+                       const double* cir, const int32_t* nc, const double* elp, const int32_t* ne, const double* u,
+                       const double* last_u, double* f, double* grad, double* c, double* J, double* cl, double* cu,
+                       double* goal_eff, int8_t* row_active, void* hip_stream)
+{
+    (void)last_u;
+    return run_batch((Handle*)handle, false, B, x0, goal, leg, cir, nc, elp, ne, u, nullptr, nullptr, nullptr,
+                     nullptr, nullptr, f, grad, c, J, cl, cu, goal_eff, row_active, hip_stream);
+}
+
+double alipmpc_last_kernel_ms(void* handle)
+{
+    Handle* h = (Handle*)handle;
+    if (!h || !h->timed) return 0.0;
+    if (hipEventSynchronize(h->ev1) != hipSuccess) return 0.0;
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, h->ev0, h->ev1) != hipSuccess) return 0.0;
+    return (double)ms;
+}
+
+const char* alipmpc_last_error(void* handle)
+{
+    Handle* h = (Handle*)handle;
+    return h ? h->err.c_str() : "null handle";
+}
+
+void alipmpc_destroy(void* handle)
+{
+    Handle* h = (Handle*)handle;
+    if (!h) return;
+    hipSetDevice(h->device);
+    if (h->own) hipStreamSynchronize(h->own);
+    if (h->dG) hipFree(h->dG);
+    if (h->dE) hipFree(h->dE);
+    if (h->stage) hipFree(h->stage);
+    if (h->ev0) hipEventDestroy(h->ev0);
+    if (h->ev1) hipEventDestroy(h->ev1);
+    if (h->own) hipStreamDestroy(h->own);
+    delete h;
+}
+
+}  // extern "C"

@@ -1,0 +1,945 @@
+/*
+ * ORACLE — TEST INFRASTRUCTURE ONLY.  CPU (C, fp64) restatement of the reference ALIP-MPC-CBF NLP and
+ * of the interior-point solve that stands in for cyipopt/IPOPT.  Mirrors oracle/np_oracle.py line by
+ * line (same formulas, same algorithm and constants) so that the numpy and C restatements check each
+ * other, and so that the CPU baseline in bench.py runs the same algorithm as the HIP kernels.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load liboracle.so, and only
+ * as the checker / reported baseline.  libalipmpc.so (the product) never links or calls it.
+ *
+ * Reference anchors (file:line in /root/reference):
+ *   constants A, B, W, M_A, M_B, dx_du, dP_du    MPC_LIP_modi.py:14-87   (generalised to any N)
+ *   select_obs                                   MPC_LIP_modi.py:325-338
+ *   cl/cu (leg parity) + detour goal             MPC_LIP_modi.py:197-271; MPC_LIP_sig_step.py:184-254
+ *   objective / gradient                         MPC_LIP_modi.py:430-465, 645-655
+ *   constraints / jacobian                       MPC_LIP_modi.py:468-583, 586-643
+ *   rollout, p_list[0]                           MPC_LIP_modi.py:102-112, 630-634
+ *   solver: IPOPT (3rd party via cyipopt, version unpinned; MPC_LIP_modi.py:274-296) — restated as a
+ *   primal-dual interior point with IPOPT's defaults (monotone mu, fraction-to-boundary, inertia
+ *   correction, filter line search) and a slack-reset restoration substitute.  See DESIGN.md.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/alipmpc.h"
+
+#define OMAXN 8
+#define OMAXV (5 * OMAXN)
+#define OMAXO ALIPMPC_MAX_OBS
+#define OMAXM (OMAXN * (5 + OMAXO))
+
+typedef struct {
+    int N, n;
+    double beta;
+    double A[5][5], B[5][3], W[3][5], MA[5][5], MB[5][5];
+    double Phi[OMAXN + 1][5][OMAXV]; /* d x_k / du */
+    double Psi[OMAXN][3][OMAXV];     /* d p_k / du */
+} oconsts;
+
+typedef struct {
+    const alipmpc_cfg* cfg;
+    const oconsts* K;
+    int N, n, m, rpk, nc, ne, modi;
+    double x0[5], goal[2], goal_orig[2];
+    double cir[OMAXO][3], elp[OMAXO][5];
+    double eqa[OMAXO], eqb[OMAXO], eqc[OMAXO], ek[OMAXO];
+    int sel_c[OMAXO], sel_e[OMAXO];
+    double cl[OMAXM], cu[OMAXM];
+    double eps_abs;
+} oprob;
+
+/* ------------------------------------------------------------------------------------------------ */
+int oracle_default_cfg(int32_t variant, int32_t N, alipmpc_cfg* c)
+{
+    memset(c, 0, sizeof(*c));
+    c->N = N;
+    c->nc_max = 6;
+    c->ne_max = 6;
+    c->variant = variant;
+    c->max_iter = 100;
+    c->precision = 0;
+    c->select_obs = 1;
+    c->detour = 1;
+    c->tol = 1e-8;
+    c->acceptable_tol = 1e-6;
+    c->dt = 0.4;
+    c->H = 1.0;
+    c->g = 9.81;
+    c->leg2_max = 0.09;
+    c->bvx_lo = 0.4;
+    c->bvx_hi = 0.8;
+    c->bvy_lo = 0.15;
+    c->bvy_hi = 0.35;
+    c->dtheta_max = M_PI / 16;
+    c->q = 1.0;
+    c->p = 0.0;
+    c->r = 50.0;
+    c->gamma = 0.2;
+    c->s = 0.024 * 180 / M_PI;
+    c->detect_r2 = 16.0;
+    c->dd_t = 2.0;
+    c->mu_init = 0.1;
+    if (variant == ALIPMPC_VARIANT_SIG_STEP) {
+        c->bvy_hi = 0.30;
+        c->p = 2.0;
+        c->r = 15.0;
+        c->gamma = 0.4;
+        c->s = 0.014 * 180 / M_PI;
+        c->select_obs = 0;
+    } else if (variant == ALIPMPC_VARIANT_DD) {
+        c->select_obs = 0;
+        c->detour = 0;
+    }
+    return 0;
+}
+
+static void mm55(double a[5][5], double b[5][5], double out[5][5])
+{
+    double t[5][5];
+    for (int i = 0; i < 5; ++i)
+        for (int j = 0; j < 5; ++j) {
+            double s = 0;
+            for (int k = 0; k < 5; ++k) s += a[i][k] * b[k][j];
+            t[i][j] = s;
+        }
+    memcpy(out, t, sizeof(t));
+}
+
+void oracle_consts(const alipmpc_cfg* cfg, oconsts* K)
+{
+    memset(K, 0, sizeof(*K));
+    double b = sqrt(cfg->g / cfg->H), T = cfg->dt;
+    double ch = cosh(b * T), sh = sinh(b * T);
+    K->beta = b;
+    K->N = cfg->N;
+    K->n = 5 * cfg->N;
+    double A[5][5] = {{ch, 0, sh / b, 0, 0}, {0, ch, 0, sh / b, 0}, {sh * b, 0, ch, 0, 0}, {0, sh * b, 0, ch, 0}, {0, 0, 0, 0, 1}};
+    double B[5][3] = {{1 - ch, 0, 0}, {0, 1 - ch, 0}, {-sh * b, 0, 0}, {0, -sh * b, 0}, {0, 0, 1}};
+    double a_ = 5.0, b_ = 1.0;
+    double D = a_ * (ch - 1) * (ch - 1) + b_ * (sh * b) * (sh * b);
+    double Ch = -a_ * (ch - 1) / D, Sh = -b_ * sh * b / D;
+    double W[3][5] = {{Ch, 0, Sh, 0, 0}, {0, Ch, 0, Sh, 0}, {0, 0, 0, 0, 1}};
+    memcpy(K->A, A, sizeof(A));
+    memcpy(K->B, B, sizeof(B));
+    memcpy(K->W, W, sizeof(W));
+    double BW[5][5];
+    for (int i = 0; i < 5; ++i)
+        for (int j = 0; j < 5; ++j) {
+            double s = 0;
+            for (int k = 0; k < 3; ++k) s += B[i][k] * W[k][j];
+            BW[i][j] = s;
+        }
+    double BWA[5][5];
+    mm55(BW, K->A, BWA);
+    for (int i = 0; i < 5; ++i)
+        for (int j = 0; j < 5; ++j) {
+            K->MA[i][j] = A[i][j] - BWA[i][j];
+            K->MB[i][j] = BW[i][j];
+        }
+    int n = K->n;
+    for (int k = 1; k <= cfg->N; ++k) {
+        for (int i = 0; i < 5; ++i)
+            for (int j = 0; j < n; ++j) {
+                double s = 0;
+                for (int t = 0; t < 5; ++t) s += K->MA[i][t] * K->Phi[k - 1][t][j];
+                K->Phi[k][i][j] = s;
+            }
+        for (int i = 0; i < 5; ++i)
+            for (int j = 0; j < 5; ++j) K->Phi[k][i][5 * (k - 1) + j] += K->MB[i][j];
+    }
+    for (int k = 0; k < cfg->N; ++k) {
+        double WA[3][5];
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 5; ++j) {
+                double s = 0;
+                for (int t = 0; t < 5; ++t) s += W[i][t] * A[t][j];
+                WA[i][j] = s;
+            }
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < n; ++j) {
+                double s = 0;
+                for (int t = 0; t < 5; ++t) s += WA[i][t] * K->Phi[k][t][j];
+                K->Psi[k][i][j] = -s;
+            }
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 5; ++j) K->Psi[k][i][5 * k + j] += W[i][j];
+    }
+}
+
+/* ------------------------------------------------------------------------------------------------ */
+/* set-up: select_obs, detour goal, cl/cu (compact reference row order) */
+static void oprob_init(oprob* P, const alipmpc_cfg* cfg, const oconsts* K, const double* x0, const double* goal,
+                       int leg, const double* cir, int nc, const double* elp, int ne)
+{
+    memset(P, 0, sizeof(*P));
+    P->cfg = cfg;
+    P->K = K;
+    P->N = cfg->N;
+    P->n = 5 * cfg->N;
+    P->modi = cfg->variant == ALIPMPC_VARIANT_MODI;
+    memcpy(P->x0, x0, 5 * sizeof(double));
+    P->goal_orig[0] = goal[0];
+    P->goal_orig[1] = goal[1];
+    for (int j = 0; j < nc; ++j) {
+        const double* c = cir + 3 * j;
+        double d = (x0[0] - c[0]) * (x0[0] - c[0]) + (x0[1] - c[1]) * (x0[1] - c[1]) - c[2] * c[2];
+        if (!cfg->select_obs || d <= cfg->detect_r2) {
+            memcpy(P->cir[P->nc], c, 3 * sizeof(double));
+            P->sel_c[P->nc++] = j;
+        }
+    }
+    for (int j = 0; j < ne; ++j) {
+        const double* e = elp + 5 * j;
+        double r = e[2] > e[3] ? e[2] : e[3];
+        double d = (x0[0] - e[0]) * (x0[0] - e[0]) + (x0[1] - e[1]) * (x0[1] - e[1]) - r * r;
+        if (!cfg->select_obs || d <= cfg->detect_r2) {
+            memcpy(P->elp[P->ne], e, 5 * sizeof(double));
+            P->sel_e[P->ne++] = j;
+        }
+    }
+    for (int j = 0; j < P->ne; ++j) {
+        const double* e = P->elp[j];
+        double ce = cos(e[4]), se = sin(e[4]);
+        P->eqa[j] = (e[3] * ce) * (e[3] * ce) + (e[2] * se) * (e[2] * se);
+        P->eqb[j] = 2 * ce * se * (e[3] * e[3] - e[2] * e[2]);
+        P->eqc[j] = (e[3] * se) * (e[3] * se) + (e[2] * ce) * (e[2] * ce);
+        P->ek[j] = (e[3] * e[2]) * (e[3] * e[2]);
+    }
+    /* detour goal (MPC_LIP_modi.py:247-271) */
+    P->goal[0] = goal[0];
+    P->goal[1] = goal[1];
+    if (cfg->detour) {
+        for (int j = 0; j < P->nc; ++j) {
+            const double* c = P->cir[j];
+            double cen = (x0[0] - c[0]) * (x0[0] - c[0]) + (x0[1] - c[1]) * (x0[1] - c[1]);
+            double gd = (x0[0] - goal[0]) * (x0[0] - goal[0]) + (x0[1] - goal[1]) * (x0[1] - goal[1]);
+            if (cen < gd && cen < 9 * c[2] * c[2]) {
+                double th = atan2(goal[1] - x0[1], goal[0] - x0[0]);
+                double al = atan2(c[1] - x0[1], c[0] - x0[0]);
+                double d = th - al;
+                if (d < 0 && fabs(d) > M_PI)
+                    d += 2 * M_PI;
+                else if (d > 0 && fabs(d) > M_PI)
+                    d -= 2 * M_PI;
+                if (fabs(d) < M_PI / 12) {
+                    double na = d < 0 ? th - M_PI / 12 : th + M_PI / 12;
+                    double rr = sqrt(gd);
+                    P->goal[0] = x0[0] + rr * cos(na);
+                    P->goal[1] = x0[1] + rr * sin(na);
+                    break;
+                }
+            }
+        }
+    }
+    /* cl / cu (MPC_LIP_modi.py:205-245) */
+    P->rpk = 4 + P->nc + P->ne + P->modi;
+    P->m = P->N * P->rpk;
+    int r = 0;
+    for (int k = 0; k < P->N; ++k) {
+        int pos_side = (leg > 0) == (k % 2 == 0);
+        double vlo = pos_side ? cfg->bvy_lo : -cfg->bvy_hi;
+        double vhi = pos_side ? cfg->bvy_hi : -cfg->bvy_lo;
+        P->cl[r] = cfg->bvx_lo;
+        P->cu[r++] = cfg->bvx_hi;
+        P->cl[r] = vlo;
+        P->cu[r++] = vhi;
+        for (int j = 0; j < P->nc + P->ne; ++j) {
+            P->cl[r] = 0.0;
+            P->cu[r++] = INFINITY;
+        }
+        P->cl[r] = 0.0;
+        P->cu[r++] = cfg->leg2_max;
+        P->cl[r] = -cfg->dtheta_max;
+        P->cu[r++] = cfg->dtheta_max;
+        if (P->modi) {
+            P->cl[r] = cfg->bvx_lo;
+            P->cu[r++] = cfg->bvx_hi;
+        }
+    }
+}
+
+/* rollout x_{i+1} = M_A x_i + M_B u_i, p_i = W(u_i - A x_i) */
+static void rollout(const oprob* P, const double* u, double X[][5], double Pp[][3])
+{
+    const oconsts* K = P->K;
+    memcpy(X[0], P->x0, 5 * sizeof(double));
+    for (int i = 0; i < P->N; ++i) {
+        const double* ui = u + 5 * i;
+        double Ax[5];
+        for (int a = 0; a < 5; ++a) {
+            double s = 0;
+            for (int b = 0; b < 5; ++b) s += K->A[a][b] * X[i][b];
+            Ax[a] = s;
+        }
+        for (int a = 0; a < 3; ++a) {
+            double s = 0;
+            for (int b = 0; b < 5; ++b) s += K->W[a][b] * (ui[b] - Ax[b]);
+            Pp[i][a] = s;
+        }
+        for (int a = 0; a < 5; ++a) {
+            double s = 0;
+            for (int b = 0; b < 5; ++b) s += K->MA[a][b] * X[i][b];
+            double t = 0;
+            for (int b = 0; b < 5; ++b) t += K->MB[a][b] * ui[b];
+            X[i + 1][a] = s + t;
+        }
+    }
+}
+
+static void oabs(const oprob* P, double x, double* v, double* d1, double* d2)
+{
+    if (P->eps_abs == 0.0) {
+        *v = fabs(x);
+        *d1 = x == 0 ? 0.0 : copysign(1.0, x);
+        *d2 = 0.0;
+    } else {
+        double r = sqrt(x * x + P->eps_abs * P->eps_abs);
+        *v = r;
+        *d1 = x / r;
+        *d2 = P->eps_abs * P->eps_abs / (r * r * r);
+    }
+}
+
+static double h_obs(const oprob* P, int j, double px, double py)
+{
+    if (j < P->nc) {
+        const double* c = P->cir[j];
+        return (px - c[0]) * (px - c[0]) + (py - c[1]) * (py - c[1]) - c[2] * c[2];
+    }
+    int e = j - P->nc;
+    double dx = px - P->elp[e][0], dy = py - P->elp[e][1];
+    return P->eqa[e] * dx * dx + P->eqb[e] * dx * dy + P->eqc[e] * dy * dy - P->ek[e];
+}
+
+static void dh_obs(const oprob* P, int j, double px, double py, double* g0, double* g1)
+{
+    if (j < P->nc) {
+        *g0 = 2 * (px - P->cir[j][0]);
+        *g1 = 2 * (py - P->cir[j][1]);
+        return;
+    }
+    int e = j - P->nc;
+    double dx = px - P->elp[e][0], dy = py - P->elp[e][1];
+    *g0 = 2 * P->eqa[e] * dx + P->eqb[e] * dy;
+    *g1 = 2 * P->eqc[e] * dy + P->eqb[e] * dx;
+}
+
+double oracle_objective(const oprob* P, const double* u)
+{
+    const alipmpc_cfg* c = P->cfg;
+    double X[OMAXN + 1][5], Pp[OMAXN][3];
+    rollout(P, u, X, Pp);
+    double f = 0;
+    for (int k = 1; k <= P->N; ++k) {
+        double dx = X[k][0] - P->goal[0], dy = X[k][1] - P->goal[1];
+        double tar = atan2(P->goal[1] - X[k][1], P->goal[0] - X[k][0]);
+        f += c->q * (dx * dx + dy * dy) + c->r * (X[k][4] - tar) * (X[k][4] - tar);
+    }
+    double dx = X[1][0] - P->goal[0], dy = X[1][1] - P->goal[1];
+    f += c->p * (dx * dx + dy * dy);
+    return f;
+}
+
+static void gradient(const oprob* P, const double* u, double* g)
+{
+    const alipmpc_cfg* c = P->cfg;
+    const oconsts* K = P->K;
+    double X[OMAXN + 1][5], Pp[OMAXN][3];
+    rollout(P, u, X, Pp);
+    int n = P->n;
+    for (int j = 0; j < n; ++j) g[j] = 0;
+    for (int k = 1; k <= P->N; ++k) {
+        double w = c->q + (k == 1 ? c->p : 0.0);
+        double ex = X[k][0] - P->goal[0], ey = X[k][1] - P->goal[1];
+        double dxg = P->goal[0] - X[k][0], dyg = P->goal[1] - X[k][1];
+        double rho2 = dxg * dxg + dyg * dyg;
+        double phi = X[k][4] - atan2(dyg, dxg);
+        for (int j = 0; j < n; ++j) {
+            double dtar = (dxg * (-K->Phi[k][1][j]) - dyg * (-K->Phi[k][0][j])) / rho2;
+            g[j] += 2 * w * (ex * K->Phi[k][0][j] + ey * K->Phi[k][1][j]) + 2 * c->r * phi * (K->Phi[k][4][j] - dtar);
+        }
+    }
+}
+
+static void constraints(const oprob* P, const double* u, double* out)
+{
+    const alipmpc_cfg* c = P->cfg;
+    double X[OMAXN + 1][5], Pp[OMAXN][3];
+    rollout(P, u, X, Pp);
+    double gm1 = c->gamma - 1.0;
+    int r = 0;
+    for (int i = 0; i < P->N; ++i) {
+        double th = X[i + 1][4], ct = cos(th), st = sin(th);
+        double vbx = ct * X[i + 1][2] + st * X[i + 1][3];
+        double vby = -st * X[i + 1][2] + ct * X[i + 1][3];
+        out[r++] = vbx;
+        out[r++] = vby;
+        for (int j = 0; j < P->nc + P->ne; ++j) out[r++] = h_obs(P, j, X[i + 1][0], X[i + 1][1]) + gm1 * h_obs(P, j, X[i][0], X[i][1]);
+        out[r++] = (X[i][0] - Pp[i][0]) * (X[i][0] - Pp[i][0]) + (X[i][1] - Pp[i][1]) * (X[i][1] - Pp[i][1]);
+        out[r++] = Pp[i][2];
+        if (P->modi) {
+            double a, d1, d2;
+            oabs(P, Pp[i][2], &a, &d1, &d2);
+            out[r++] = c->s * a + vbx;
+        }
+    }
+}
+
+static void jacobian(const oprob* P, const double* u, double* J /* m x n */)
+{
+    const alipmpc_cfg* c = P->cfg;
+    const oconsts* K = P->K;
+    double X[OMAXN + 1][5], Pp[OMAXN][3];
+    rollout(P, u, X, Pp);
+    int n = P->n;
+    double gm1 = c->gamma - 1.0;
+    int r = 0;
+    for (int i = 0; i < P->N; ++i) {
+        const double(*F)[OMAXV] = K->Phi[i + 1];
+        const double(*F0)[OMAXV] = K->Phi[i];
+        const double(*Ps)[OMAXV] = K->Psi[i];
+        double th = X[i + 1][4], vx = X[i + 1][2], vy = X[i + 1][3], ct = cos(th), st = sin(th);
+        double a3 = -st * vx + ct * vy, b3 = -ct * vx - st * vy;
+        double* rbx = J + (size_t)r * n;
+        for (int j = 0; j < n; ++j) rbx[j] = ct * F[2][j] + st * F[3][j] + a3 * F[4][j];
+        r++;
+        for (int j = 0; j < n; ++j) J[(size_t)r * n + j] = -st * F[2][j] + ct * F[3][j] + b3 * F[4][j];
+        r++;
+        for (int o = 0; o < P->nc + P->ne; ++o) {
+            double g0, g1, h0, h1;
+            dh_obs(P, o, X[i + 1][0], X[i + 1][1], &g0, &g1);
+            dh_obs(P, o, X[i][0], X[i][1], &h0, &h1);
+            for (int j = 0; j < n; ++j) J[(size_t)r * n + j] = g0 * F[0][j] + g1 * F[1][j] + gm1 * (h0 * F0[0][j] + h1 * F0[1][j]);
+            r++;
+        }
+        double ex = X[i][0] - Pp[i][0], ey = X[i][1] - Pp[i][1];
+        for (int j = 0; j < n; ++j) J[(size_t)r * n + j] = 2 * ex * (F0[0][j] - Ps[0][j]) + 2 * ey * (F0[1][j] - Ps[1][j]);
+        r++;
+        for (int j = 0; j < n; ++j) J[(size_t)r * n + j] = Ps[2][j];
+        r++;
+        if (P->modi) {
+            double a, d1, d2;
+            oabs(P, Pp[i][2], &a, &d1, &d2);
+            for (int j = 0; j < n; ++j) J[(size_t)r * n + j] = c->s * d1 * Ps[2][j] + rbx[j];
+            r++;
+        }
+    }
+}
+
+/* exact Hessian of L = f - y^T c */
+static void hessian(const oprob* P, const double* u, const double* y, double* H /* n x n */)
+{
+    const alipmpc_cfg* c = P->cfg;
+    const oconsts* K = P->K;
+    double X[OMAXN + 1][5], Pp[OMAXN][3];
+    rollout(P, u, X, Pp);
+    int n = P->n, N = P->N;
+    double Hl[OMAXN + 1][5][5];
+    memset(Hl, 0, sizeof(Hl));
+    for (int i = 0; i < n * n; ++i) H[i] = 0;
+    for (int k = 1; k <= N; ++k) {
+        double w = c->q + (k == 1 ? c->p : 0.0);
+        Hl[k][0][0] += 2 * w;
+        Hl[k][1][1] += 2 * w;
+        double dxg = P->goal[0] - X[k][0], dyg = P->goal[1] - X[k][1];
+        double rho2 = dxg * dxg + dyg * dyg;
+        double phi = X[k][4] - atan2(dyg, dxg);
+        double gp[3] = {-dyg / rho2, dxg / rho2, 1.0};
+        int idx[3] = {0, 1, 4};
+        for (int a = 0; a < 3; ++a)
+            for (int b = 0; b < 3; ++b) Hl[k][idx[a]][idx[b]] += 2 * c->r * gp[a] * gp[b];
+        double r4 = rho2 * rho2;
+        double h00 = 2 * dxg * dyg / r4, h01 = (dyg * dyg - dxg * dxg) / r4, h11 = -2 * dxg * dyg / r4;
+        Hl[k][0][0] += 2 * c->r * phi * (-h00);
+        Hl[k][0][1] += 2 * c->r * phi * (-h01);
+        Hl[k][1][0] += 2 * c->r * phi * (-h01);
+        Hl[k][1][1] += 2 * c->r * phi * (-h11);
+    }
+    int nob = P->nc + P->ne;
+    double gm1 = c->gamma - 1.0;
+    for (int i = 0; i < N; ++i) {
+        const double* yk = y + i * P->rpk;
+        double th = X[i + 1][4], vx = X[i + 1][2], vy = X[i + 1][3], ct = cos(th), st = sin(th);
+        double vbx = ct * vx + st * vy, vby = -st * vx + ct * vy;
+        double wbx = yk[0] + (P->modi ? yk[P->rpk - 1] : 0.0), wby = yk[1];
+        double hvx = -wbx * (-st) - wby * (-ct);
+        double hvy = -wbx * ct - wby * (-st);
+        Hl[i + 1][2][4] += hvx;
+        Hl[i + 1][4][2] += hvx;
+        Hl[i + 1][3][4] += hvy;
+        Hl[i + 1][4][3] += hvy;
+        Hl[i + 1][4][4] += -wbx * (-vbx) - wby * (-vby);
+        for (int o = 0; o < nob; ++o) {
+            double wj = yk[2 + o];
+            double q00, q01, q11;
+            if (o < P->nc) {
+                q00 = 2;
+                q01 = 0;
+                q11 = 2;
+            } else {
+                int e = o - P->nc;
+                q00 = 2 * P->eqa[e];
+                q01 = P->eqb[e];
+                q11 = 2 * P->eqc[e];
+            }
+            Hl[i + 1][0][0] += -wj * q00;
+            Hl[i + 1][0][1] += -wj * q01;
+            Hl[i + 1][1][0] += -wj * q01;
+            Hl[i + 1][1][1] += -wj * q11;
+            if (i >= 1) {
+                Hl[i][0][0] += -wj * gm1 * q00;
+                Hl[i][0][1] += -wj * gm1 * q01;
+                Hl[i][1][0] += -wj * gm1 * q01;
+                Hl[i][1][1] += -wj * gm1 * q11;
+            }
+        }
+        double wl = yk[2 + nob];
+        for (int a = 0; a < n; ++a) {
+            double e0a = K->Phi[i][0][a] - K->Psi[i][0][a], e1a = K->Phi[i][1][a] - K->Psi[i][1][a];
+            for (int b = 0; b < n; ++b) {
+                double e0b = K->Phi[i][0][b] - K->Psi[i][0][b], e1b = K->Phi[i][1][b] - K->Psi[i][1][b];
+                H[a * n + b] += -wl * 2 * (e0a * e0b + e1a * e1b);
+            }
+        }
+        if (P->modi) {
+            double av, d1, d2;
+            oabs(P, Pp[i][2], &av, &d1, &d2);
+            if (d2 != 0.0) {
+                double w = -yk[P->rpk - 1] * c->s * d2;
+                for (int a = 0; a < n; ++a)
+                    for (int b = 0; b < n; ++b) H[a * n + b] += w * K->Psi[i][2][a] * K->Psi[i][2][b];
+            }
+        }
+    }
+    for (int k = 1; k <= N; ++k) {
+        double T[5][OMAXV];
+        for (int a = 0; a < 5; ++a)
+            for (int j = 0; j < n; ++j) {
+                double s = 0;
+                for (int b = 0; b < 5; ++b) s += Hl[k][a][b] * K->Phi[k][b][j];
+                T[a][j] = s;
+            }
+        for (int a = 0; a < n; ++a)
+            for (int b = 0; b < n; ++b) {
+                double s = 0;
+                for (int t = 0; t < 5; ++t) s += K->Phi[k][t][a] * T[t][b];
+                H[a * n + b] += s;
+            }
+    }
+}
+
+/* ------------------------------------------------------------------------------------------------ */
+static int chol(double* A, int n)
+{
+    for (int j = 0; j < n; ++j) {
+        double d = A[j * n + j];
+        for (int k = 0; k < j; ++k) d -= A[j * n + k] * A[j * n + k];
+        if (!(d > 0)) return 0;
+        d = sqrt(d);
+        A[j * n + j] = d;
+        for (int i = j + 1; i < n; ++i) {
+            double s = A[i * n + j];
+            for (int k = 0; k < j; ++k) s -= A[i * n + k] * A[j * n + k];
+            A[i * n + j] = s / d;
+        }
+    }
+    return 1;
+}
+
+static void cholsolve(const double* L, int n, double* b)
+{
+    for (int i = 0; i < n; ++i) {
+        double s = b[i];
+        for (int k = 0; k < i; ++k) s -= L[i * n + k] * b[k];
+        b[i] = s / L[i * n + i];
+    }
+    for (int i = n - 1; i >= 0; --i) {
+        double s = b[i];
+        for (int k = i + 1; k < n; ++k) s -= L[k * n + i] * b[k];
+        b[i] = s / L[i * n + i];
+    }
+}
+
+static void push_slacks(const double* c, const double* cl, const double* cu, int m, double* s)
+{
+    for (int i = 0; i < m; ++i) {
+        int hl = isfinite(cl[i]), hu = isfinite(cu[i]);
+        double v = c[i];
+        double pl = 0, pu = 0;
+        if (hl) pl = fmin(1e-2 * fmax(1.0, fabs(cl[i])), 1e-2 * (cu[i] - cl[i]));
+        if (hu) pu = fmin(1e-2 * fmax(1.0, fabs(cu[i])), 1e-2 * (cu[i] - cl[i]));
+        if (hl && hu)
+            v = fmin(fmax(v, cl[i] + pl), cu[i] - pu);
+        else if (hl)
+            v = fmax(v, cl[i] + pl);
+        else if (hu)
+            v = fmin(v, cu[i] - pu);
+        s[i] = v;
+    }
+}
+
+static double eps_abs_of_mu(double mu) { return 0.1 * sqrt(mu); }
+
+static double barrier(double f, const double* s, const double* cl, const double* cu, int m, double mu)
+{
+    double acc = 0;
+    for (int i = 0; i < m; ++i) {
+        if (isfinite(cl[i])) {
+            double d = s[i] - cl[i];
+            if (!(d > 0)) return INFINITY;
+            acc += log(d);
+        }
+        if (isfinite(cu[i])) {
+            double d = cu[i] - s[i];
+            if (!(d > 0)) return INFINITY;
+            acc += log(d);
+        }
+    }
+    return f - mu * acc;
+}
+
+typedef struct {
+    int iters, status, restorations;
+} osolve_info;
+
+/* Primal-dual interior point with IPOPT's filter line search; mirrors np_oracle.solve. */
+static void osolve(oprob* P, const double* u0, double* u, osolve_info* info)
+{
+    const alipmpc_cfg* cfg = P->cfg;
+    const int n = P->n, m = P->m;
+    const int smooth = P->modi;
+    double cl[OMAXM], cu[OMAXM];
+    int hl[OMAXM], hu[OMAXM];
+    int nb = 0;
+    for (int i = 0; i < m; ++i) {
+        hl[i] = isfinite(P->cl[i]);
+        hu[i] = isfinite(P->cu[i]);
+        nb += hl[i] + hu[i];
+        cl[i] = hl[i] ? P->cl[i] - 1e-8 * fmax(1.0, fabs(P->cl[i])) : -INFINITY;
+        cu[i] = hu[i] ? P->cu[i] + 1e-8 * fmax(1.0, fabs(P->cu[i])) : INFINITY;
+    }
+    memcpy(u, u0, n * sizeof(double));
+    double mu = cfg->mu_init;
+    P->eps_abs = smooth ? eps_abs_of_mu(mu) : 0.0;
+    double c[OMAXM], s[OMAXM], zl[OMAXM], zu[OMAXM];
+    constraints(P, u, c);
+    push_slacks(c, cl, cu, m, s);
+    for (int i = 0; i < m; ++i) {
+        zl[i] = hl[i] ? 1.0 : 0.0;
+        zu[i] = hu[i] ? 1.0 : 0.0;
+    }
+    double dw_last = 0.0;
+    int status = -1, it = 0, n_rest = 0;
+    double e0 = INFINITY;
+    double th0 = 0;
+    for (int i = 0; i < m; ++i) th0 += fabs(c[i] - s[i]);
+    const double theta_max = 1e4 * fmax(1.0, th0), theta_min = 1e-4 * fmax(1.0, th0);
+    const int maxf = cfg->max_iter + 2;
+    double* ft = (double*)malloc(sizeof(double) * 2 * maxf);
+    int nf = 0;
+    static const double gth = 1e-5, gph = 1e-8, sth = 1.1, sph = 2.3, eta = 1e-8, gal = 0.05;
+    double gf[OMAXV], J[OMAXM * OMAXV], H[OMAXV * OMAXV], Kmat[OMAXV * OMAXV], rhs[OMAXV], y[OMAXM];
+    double dl[OMAXM], du[OMAXM], rc[OMAXM], Sig[OMAXM], dU[OMAXV], dS[OMAXM], dZl[OMAXM], dZu[OMAXM];
+    double ut[OMAXV], st[OMAXM], ct[OMAXM];
+    for (it = 0; it <= cfg->max_iter; ++it) {
+        double f = oracle_objective(P, u);
+        gradient(P, u, gf);
+        jacobian(P, u, J);
+        double nz = 0;
+        for (int i = 0; i < m; ++i) {
+            dl[i] = hl[i] ? s[i] - cl[i] : 1.0;
+            du[i] = hu[i] ? cu[i] - s[i] : 1.0;
+            y[i] = zl[i] - zu[i];
+            rc[i] = c[i] - s[i];
+            nz += fabs(zl[i]) + fabs(zu[i]);
+        }
+        double ru_max = 0;
+        for (int j = 0; j < n; ++j) {
+            double a = gf[j];
+            for (int i = 0; i < m; ++i) a -= J[i * n + j] * y[i];
+            ru_max = fmax(ru_max, fabs(a));
+        }
+        double rc_max = 0;
+        for (int i = 0; i < m; ++i) rc_max = fmax(rc_max, fabs(rc[i]));
+        double sd = fmax(100.0, nz / (m + n)) / 100.0;
+        double sc = fmax(100.0, nz / (nb > 0 ? nb : 1)) / 100.0;
+#define ERR(muv)                                                                \
+    ({                                                                          \
+        double comp_ = 0;                                                       \
+        for (int i_ = 0; i_ < m; ++i_) {                                        \
+            if (hl[i_]) comp_ = fmax(comp_, fabs(dl[i_] * zl[i_] - (muv)));     \
+            if (hu[i_]) comp_ = fmax(comp_, fabs(du[i_] * zu[i_] - (muv)));     \
+        }                                                                       \
+        fmax(fmax(ru_max / sd, rc_max), comp_ / sc);                            \
+    })
+        e0 = ERR(0.0);
+        if (e0 <= cfg->tol) {
+            status = 0;
+            break;
+        }
+        if (it == cfg->max_iter) break;
+        double mu_min = cfg->tol / 10.0, mu_old = mu;
+        for (int t = 0; t < 8; ++t) {
+            if (ERR(mu) <= 10.0 * mu && mu > mu_min)
+                mu = fmax(mu_min, fmin(0.2 * mu, pow(mu, 1.5)));
+            else
+                break;
+        }
+        if (mu != mu_old) {
+            nf = 0;
+            if (smooth) {
+                P->eps_abs = eps_abs_of_mu(mu);
+                f = oracle_objective(P, u);
+                gradient(P, u, gf);
+                jacobian(P, u, J);
+                constraints(P, u, c);
+                for (int i = 0; i < m; ++i) rc[i] = c[i] - s[i];
+            }
+        }
+        double tau = fmax(0.99, 1.0 - mu);
+        for (int i = 0; i < m; ++i) Sig[i] = (hl[i] ? zl[i] / dl[i] : 0.0) + (hu[i] ? zu[i] / du[i] : 0.0);
+        hessian(P, u, y, H);
+        for (int a = 0; a < n; ++a) {
+            for (int b = 0; b < n; ++b) {
+                double acc = 0;
+                for (int i = 0; i < m; ++i) acc += J[i * n + a] * Sig[i] * J[i * n + b];
+                Kmat[a * n + b] = H[a * n + b] + acc;
+            }
+            double acc = -gf[a];
+            for (int i = 0; i < m; ++i) {
+                double w = (hl[i] ? mu / dl[i] : 0.0) - (hu[i] ? mu / du[i] : 0.0) - Sig[i] * rc[i];
+                acc += J[i * n + a] * w;
+            }
+            rhs[a] = acc;
+        }
+        double L[OMAXV * OMAXV];
+        double dw = 0.0;
+        memcpy(L, Kmat, sizeof(double) * n * n);
+        if (!chol(L, n)) {
+            dw = dw_last == 0 ? 1e-4 : fmax(1e-20, dw_last / 3.0);
+            for (;;) {
+                memcpy(L, Kmat, sizeof(double) * n * n);
+                for (int a = 0; a < n; ++a) L[a * n + a] += dw;
+                if (chol(L, n)) break;
+                dw *= dw_last == 0 ? 100.0 : 8.0;
+                if (dw > 1e40) break;
+            }
+            dw_last = dw;
+        }
+        memcpy(dU, rhs, sizeof(double) * n);
+        cholsolve(L, n, dU);
+        for (int i = 0; i < m; ++i) {
+            double a = rc[i];
+            for (int j = 0; j < n; ++j) a += J[i * n + j] * dU[j];
+            dS[i] = a;
+            dZl[i] = hl[i] ? mu / dl[i] - zl[i] - zl[i] / dl[i] * dS[i] : 0.0;
+            dZu[i] = hu[i] ? mu / du[i] - zu[i] + zu[i] / du[i] * dS[i] : 0.0;
+        }
+        double ap = 1.0, az = 1.0;
+        for (int i = 0; i < m; ++i) {
+            if (hl[i] && dS[i] < 0) ap = fmin(ap, -tau * dl[i] / dS[i]);
+            if (hu[i] && dS[i] > 0) ap = fmin(ap, tau * du[i] / dS[i]);
+        }
+        for (int i = 0; i < m; ++i) {
+            if (hl[i] && dZl[i] < 0) az = fmin(az, -tau * zl[i] / dZl[i]);
+            if (hu[i] && dZu[i] < 0) az = fmin(az, -tau * zu[i] / dZu[i]);
+        }
+        /* filter line search */
+        double theta = 0;
+        for (int i = 0; i < m; ++i) theta += fabs(rc[i]);
+        double phi = barrier(f, s, cl, cu, m, mu);
+        double gphi = 0, sl = 0, su = 0;
+        for (int j = 0; j < n; ++j) gphi += gf[j] * dU[j];
+        for (int i = 0; i < m; ++i) {
+            if (hl[i]) sl += dS[i] / dl[i];
+            if (hu[i]) su += dS[i] / du[i];
+        }
+        gphi -= mu * (sl - su);
+        double amin;
+        if (gphi < 0) {
+            amin = fmin(gth, gph * theta / -gphi);
+            if (theta <= theta_min) amin = fmin(amin, pow(theta, sth) / pow(-gphi, sph));
+        } else
+            amin = gth;
+        amin *= gal;
+        double a = ap;
+        int accepted = 0, ftype = 0;
+        while (a >= amin) {
+            for (int j = 0; j < n; ++j) ut[j] = u[j] + a * dU[j];
+            for (int i = 0; i < m; ++i) st[i] = s[i] + a * dS[i];
+            constraints(P, ut, ct);
+            double ftv = oracle_objective(P, ut);
+            double tht = 0;
+            for (int i = 0; i < m; ++i) tht += fabs(ct[i] - st[i]);
+            double pht = barrier(ftv, st, cl, cu, m, mu);
+            int ok = isfinite(pht) && tht < theta_max;
+            for (int q = 0; ok && q < nf; ++q)
+                if (!(tht < ft[2 * q] || pht < ft[2 * q + 1])) ok = 0;
+            if (ok) {
+                int switching = gphi < 0 && a * pow(-gphi, sph) > pow(theta, sth);
+                if (switching && theta <= theta_min) {
+                    if (pht <= phi + eta * a * gphi) {
+                        accepted = 1;
+                        ftype = 1;
+                    }
+                } else if (tht <= (1 - gth) * theta || pht <= phi - gph * theta) {
+                    accepted = 1;
+                    ftype = 0;
+                }
+            }
+            if (accepted) break;
+            a *= 0.5;
+        }
+        if (accepted) {
+            if (!ftype && nf < maxf) {
+                ft[2 * nf] = (1 - gth) * theta;
+                ft[2 * nf + 1] = phi - gph * theta;
+                nf++;
+            }
+            memcpy(u, ut, sizeof(double) * n);
+            memcpy(s, st, sizeof(double) * m);
+            memcpy(c, ct, sizeof(double) * m);
+        } else {
+            n_rest++;
+            a = fmax(a, amin);
+            for (int j = 0; j < n; ++j) u[j] += a * dU[j];
+            constraints(P, u, c);
+            push_slacks(c, cl, cu, m, s);
+            nf = 0;
+        }
+        for (int i = 0; i < m; ++i) {
+            zl[i] += az * dZl[i];
+            zu[i] += az * dZu[i];
+            if (hl[i]) {
+                double d = s[i] - cl[i];
+                zl[i] = fmin(fmax(zl[i], mu / (1e10 * d)), 1e10 * mu / d);
+            } else
+                zl[i] = 0;
+            if (hu[i]) {
+                double d = cu[i] - s[i];
+                zu[i] = fmin(fmax(zu[i], mu / (1e10 * d)), 1e10 * mu / d);
+            } else
+                zu[i] = 0;
+        }
+#undef ERR
+    }
+    free(ft);
+    P->eps_abs = 0.0;
+    if (status != 0) {
+        constraints(P, u, c);
+        double viol = 0;
+        for (int i = 0; i < m; ++i) {
+            if (hl[i]) viol = fmax(viol, P->cl[i] - c[i]);
+            if (hu[i]) viol = fmax(viol, c[i] - P->cu[i]);
+        }
+        if (e0 <= cfg->acceptable_tol)
+            status = 1;
+        else if (viol > 1e-4)
+            status = 2;
+    }
+    info->iters = it;
+    info->status = status;
+    info->restorations = n_rest;
+}
+
+/* ------------------------------------------------------------------------------------------------ */
+/* batch entry points (same argument meaning as alipmpc_solve_batch / alipmpc_eval_batch, host memory) */
+int oracle_rows_per_step(const alipmpc_cfg* cfg)
+{
+    return 4 + cfg->nc_max + cfg->ne_max + (cfg->variant == ALIPMPC_VARIANT_MODI);
+}
+
+int oracle_solve_batch(const alipmpc_cfg* cfg, int64_t B, const double* x0, const double* goal, const int8_t* leg,
+                       const double* cir, const int32_t* nc, const double* elp, const int32_t* ne, const double* u0,
+                       double* u_out, double* foot_out, double* x_pred, int32_t* status, int32_t* iters,
+                       int32_t* restorations, int nthreads)
+{
+    if (cfg->variant == ALIPMPC_VARIANT_DD || cfg->N < 1 || cfg->N > OMAXN) return ALIPMPC_EUNSUPPORTED;
+    oconsts* K = (oconsts*)malloc(sizeof(oconsts));
+    oracle_consts(cfg, K);
+    const int n = 5 * cfg->N;
+#pragma omp parallel for schedule(dynamic, 4) num_threads(nthreads > 0 ? nthreads : 1)
+    for (int64_t b = 0; b < B; ++b) {
+        oprob* P = (oprob*)malloc(sizeof(oprob));
+        oprob_init(P, cfg, K, x0 + 5 * b, goal + 2 * b, leg[b], cir + (size_t)3 * cfg->nc_max * b, nc[b],
+                   elp ? elp + (size_t)5 * cfg->ne_max * b : NULL, ne ? ne[b] : 0);
+        double u[OMAXV];
+        osolve_info info;
+        osolve(P, u0 + (size_t)n * b, u, &info);
+        if (u_out) memcpy(u_out + (size_t)n * b, u, sizeof(double) * n);
+        double X[OMAXN + 1][5], Pp[OMAXN][3];
+        rollout(P, u, X, Pp);
+        if (foot_out) memcpy(foot_out + 3 * b, Pp[0], 3 * sizeof(double));
+        if (x_pred)
+            for (int k = 0; k < cfg->N; ++k) memcpy(x_pred + ((size_t)b * cfg->N + k) * 5, X[k + 1], 5 * sizeof(double));
+        if (status) status[b] = info.status;
+        if (iters) iters[b] = info.iters;
+        if (restorations) restorations[b] = info.restorations;
+        free(P);
+    }
+    free(K);
+    return 0;
+}
+
+int oracle_eval_batch(const alipmpc_cfg* cfg, int64_t B, const double* x0, const double* goal, const int8_t* leg,
+                      const double* cir, const int32_t* nc, const double* elp, const int32_t* ne, const double* u,
+                      double* f, double* grad, double* c, double* J, double* cl, double* cu, double* goal_eff,
+                      int8_t* row_active)
+{
+    if (cfg->variant == ALIPMPC_VARIANT_DD || cfg->N < 1 || cfg->N > OMAXN) return ALIPMPC_EUNSUPPORTED;
+    oconsts* K = (oconsts*)malloc(sizeof(oconsts));
+    oracle_consts(cfg, K);
+    const int n = 5 * cfg->N;
+    const int rps = oracle_rows_per_step(cfg), mmax = cfg->N * rps;
+    oprob* P = (oprob*)malloc(sizeof(oprob));
+    double* Jc = (double*)malloc(sizeof(double) * OMAXM * OMAXV);
+    double cc[OMAXM];
+    for (int64_t b = 0; b < B; ++b) {
+        oprob_init(P, cfg, K, x0 + 5 * b, goal + 2 * b, leg[b], cir + (size_t)3 * cfg->nc_max * b, nc[b],
+                   elp ? elp + (size_t)5 * cfg->ne_max * b : NULL, ne ? ne[b] : 0);
+        const double* ub = u + (size_t)n * b;
+        if (f) f[b] = oracle_objective(P, ub);
+        if (grad) gradient(P, ub, grad + (size_t)n * b);
+        constraints(P, ub, cc);
+        jacobian(P, ub, Jc);
+        /* scatter compact rows into the padded layout */
+        for (int k = 0; k < cfg->N; ++k) {
+            int src = k * P->rpk, dst = k * rps;
+            int map[5 + 2 * OMAXO];
+            int q = 0;
+            map[q++] = dst + 0;
+            map[q++] = dst + 1;
+            for (int j = 0; j < P->nc; ++j) map[q++] = dst + 2 + j;
+            for (int j = 0; j < P->ne; ++j) map[q++] = dst + 2 + cfg->nc_max + j;
+            map[q++] = dst + 2 + cfg->nc_max + cfg->ne_max;
+            map[q++] = dst + 3 + cfg->nc_max + cfg->ne_max;
+            if (P->modi) map[q++] = dst + 4 + cfg->nc_max + cfg->ne_max;
+            for (int r = dst; r < dst + rps; ++r) {
+                if (c) c[(size_t)b * mmax + r] = 0;
+                if (J)
+                    for (int j = 0; j < n; ++j) J[((size_t)b * mmax + r) * n + j] = 0;
+                if (cl) cl[(size_t)b * mmax + r] = -INFINITY;
+                if (cu) cu[(size_t)b * mmax + r] = INFINITY;
+                if (row_active) row_active[(size_t)b * mmax + r] = 0;
+            }
+            for (int t = 0; t < q; ++t) {
+                int r = map[t];
+                if (c) c[(size_t)b * mmax + r] = cc[src + t];
+                if (J) memcpy(J + ((size_t)b * mmax + r) * n, Jc + (size_t)(src + t) * n, sizeof(double) * n);
+                if (cl) cl[(size_t)b * mmax + r] = P->cl[src + t];
+                if (cu) cu[(size_t)b * mmax + r] = P->cu[src + t];
+                if (row_active) row_active[(size_t)b * mmax + r] = 1;
+            }
+        }
+        if (goal_eff) {
+            goal_eff[2 * b] = P->goal[0];
+            goal_eff[2 * b + 1] = P->goal[1];
+        }
+    }
+    free(Jc);
+    free(P);
+    free(K);
+    return 0;
+}
