@@ -70,7 +70,7 @@ extern "C" {
 #define ALIPMPC_EUNSUPPORTED (-4)
 
 #define ALIPMPC_MAX_N 6      /* horizon limit of the kernels (n = 5N <= 32 -> two 16-column MFMA tiles) */
-#define ALIPMPC_MAX_OBS 16   /* nc_max + ne_max limit */
+#define ALIPMPC_MAX_OBS 24   /* nc_max + ne_max limit (and N * rows_per_step <= 128) */
 
 typedef struct alipmpc_cfg {
     int32_t N;          /* horizon (reference: step = 3) */

@@ -40,6 +40,7 @@ constexpr int WAVE = 64;
 constexpr int WAVES_PER_BLOCK = 4;
 constexpr int MAX_ROWS = 128;        // padded constraint rows per instance (2 per lane)
 constexpr int FILTER_CAP = 128;      // 2 filter entries per lane
+constexpr int REST_FAIL = 6;         // restoration events with violation > 1e-4 -> status 2
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
@@ -51,6 +52,8 @@ struct KP {
     double tol, acc_tol, q, p, r, gm1, s, detect_r2, leg2, bvx_lo, bvx_hi, bvy_lo, bvy_hi, dth, mu_init;
     const double* G;   // NG x NCP
     const double* E;   // NG x 5
+    const double* Gu;  // NG x NCPU : u-parametrisation V = Eu x0 + Gu u (warm start u0 -> p0)
+    const double* Eu;  // NG x 5
     long long B;
     const double* x0;
     const double* goal;
@@ -83,9 +86,12 @@ enum RowType { R_VBX = 0, R_VBY, R_CIR, R_ELP, R_LEG, R_DTH, R_FEN, R_NONE };
 
 template <int N>
 struct Dim {
-    static constexpr int n = 5 * N;
+    static constexpr int n = 3 * N;     // decision = footholds p_0..p_{N-1} (see build_tables)
     static constexpr int NT = (n + 15) / 16;
     static constexpr int NCP = 16 * NT;
+    static constexpr int nu = 5 * N;    // the reference's decision u (eval / warm start)
+    static constexpr int NTU = (nu + 15) / 16;
+    static constexpr int NCPU = 16 * NTU;
     static constexpr int NG = 8 * (N + 1);
     static constexpr int KLD = NCP + 1;
 };
@@ -510,7 +516,7 @@ __device__ __forceinline__ double jrow_col(const double* rcoef, const uint8_t* r
 // ------------------------------------------------------------------------------------------------
 // instance prologue: load inputs, select_obs, detour goal, ellipse forms, V = E x0 + G u0
 // ------------------------------------------------------------------------------------------------
-template <int N>
+template <int N, bool FROM_U>
 __device__ void prologue(const KP& P, const WS<N>& w, const double* G, const double* E, long long b, double& gxg,
                          double& gyg, int& legv, double& uj)
 {
@@ -606,12 +612,41 @@ __device__ void prologue(const KP& P, const WS<N>& w, const double* G, const dou
             gyg = bcast(ny, first);
         }
     }
-    // V = E x0 + G u0
-    uj = lane < D::n ? P.u0[(size_t)b * D::n + lane] : 0.0;
-    double xv = lane < 5 ? x0[lane] : 0.0;
+    // FROM_U (eval): V = E x0 + G u with the u-tables staged in LDS.
+    // solve: warm start p0 = rows p_k of (Eu x0 + Gu u0) — the rollout of the reference's u0 — then
+    // V = E x0 + G p0 with the foothold tables.
+    constexpr int nu = D::nu;
+    const double u0v = lane < nu ? P.u0[(size_t)b * nu + lane] : 0.0;
+    const double xv = lane < 5 ? x0[lane] : 0.0;
     double xb[5];
 #pragma unroll
     for (int c = 0; c < 5; ++c) xb[c] = bcast(xv, c);
+    if (lane < nu) w.Vt[lane] = u0v;
+    wave_sync();
+    if (FROM_U) {
+        for (int t = lane; t < D::NG; t += WAVE) {
+            double v = 0.0;
+#pragma unroll
+            for (int c = 0; c < 5; ++c) v += E[t * 5 + c] * xb[c];
+            const double* gr = G + t * D::NCPU;
+#pragma unroll
+            for (int j = 0; j < nu; ++j) v += gr[j] * w.Vt[j];
+            w.V[t] = v;
+        }
+        uj = 0.0;
+        wave_sync();
+        return;
+    }
+    if (lane < D::n) {
+        const int t = 8 * (lane / 3) + 5 + lane % 3;      // generator row of p_k[c]
+        double v = 0.0;
+#pragma unroll
+        for (int c = 0; c < 5; ++c) v += P.Eu[t * 5 + c] * xb[c];
+        const double* gr = P.Gu + (size_t)t * D::NCPU;
+        for (int j = 0; j < nu; ++j) v += gr[j] * w.Vt[j];
+        uj = v;
+    }
+    wave_sync();
     if (lane < D::n) w.Vt[lane] = uj;
     wave_sync();
     for (int t = lane; t < D::NG; t += WAVE) {
@@ -681,7 +716,7 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
 
     double gxg, gyg, uj;
     int legv;
-    prologue<N>(P, w, G, E, b, gxg, gyg, legv, uj);
+    prologue<N, false>(P, w, G, E, b, gxg, gyg, legv, uj);
     const int nc_sel = w.nsel[0], ne_sel = w.nsel[1];
     const int g4 = lane >> 4, col = lane & 15;
 
@@ -725,7 +760,7 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
     double fth[2] = {INFINITY, INFINITY}, fph[2] = {INFINITY, INFINITY};
     int nf = 0;
     double dw_last = 0.0;
-    int status = -1, it = 0;
+    int status = -1, it = 0, n_rest = 0;
     double e0 = INFINITY;
     const double gth = 1e-5, gph = 1e-8, sth = 1.1, sph = 2.3, eta = 1e-8, gal = 0.05;
 
@@ -1072,7 +1107,6 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
                 nf++;
             }
             for (int t = lane; t < NG; t += WAVE) w.V[t] = w.Vt[t];
-            uj += a * xv;
 #pragma unroll
             for (int q = 0; q < RPL; ++q) {
                 sr[q] += a * dS[q];
@@ -1082,7 +1116,6 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
             // restoration substitute: shortest tried step, slacks reset onto c(u), filter reset
             a = fmax(a, amin);
             for (int t = lane; t < NG; t += WAVE) w.V[t] += a * w.dV[t];
-            uj += a * xv;
             wave_sync();
             state_pass<N, false>(P, w.V, w.CT, w.ST, w.gfg, gxg, gyg);
             wave_sync();
@@ -1101,6 +1134,20 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
                 sr[q] = v;
             }
             nf = 0;
+            // infeasibility detection (stands in for IPOPT's failed restoration phase)
+            n_rest++;
+            double viol = 0.0;
+#pragma unroll
+            for (int q = 0; q < RPL; ++q) {
+                if (hl[q]) viol = fmax(viol, clo[q] - cr[q]);
+                if (hu[q]) viol = fmax(viol, cr[q] - cuo[q]);
+            }
+            viol = wmax(viol);
+            if (n_rest >= REST_FAIL && viol > 1e-4) {
+                status = 2;
+                it++;
+                break;
+            }
         }
 #pragma unroll
         for (int q = 0; q < RPL; ++q) {
@@ -1123,7 +1170,7 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
     }
     // ---- status + outputs (violation measured on the reference's exact |.|)
     wave_sync();
-    if (status != 0) {
+    if (status != 0 && status != 2) {
         state_pass<N, false>(P, w.V, w.CT, w.ST, w.gfg, gxg, gyg);
         wave_sync();
         double viol = 0.0;
@@ -1139,7 +1186,8 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
         else if (viol > 1e-4)
             status = 2;
     }
-    if (lane < n) P.u_out[(size_t)b * n + lane] = uj;
+    // canonical u: u_k = x_{k+1} (W u_k = p_k since W B = I) — the reference's "desired next state"
+    if (lane < 5 * N) P.u_out[(size_t)b * 5 * N + lane] = w.V[gx(lane / 5 + 1, lane % 5)];
     if (P.foot_out && lane < 3) P.foot_out[3 * b + lane] = w.V[gp(0, lane)];
     if (P.x_pred && lane < 5 * N) P.x_pred[(size_t)b * 5 * N + lane] = w.V[gx(lane / 5 + 1, lane % 5)];
     if (lane == 0) {
@@ -1155,9 +1203,9 @@ template <int N>
 __global__ __launch_bounds__(256, 4) void eval_kernel(KP Pv)
 {
     using D = Dim<N>;
-    constexpr int n = D::n;
-    constexpr int NT = D::NT;
-    constexpr int NCP = D::NCP;
+    constexpr int n = D::nu;       // the reference callbacks are functions of u
+    constexpr int NT = D::NTU;
+    constexpr int NCP = D::NCPU;
     constexpr int NG = D::NG;
     constexpr int RPL = 2;
     extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -1178,7 +1226,7 @@ __global__ __launch_bounds__(256, 4) void eval_kernel(KP Pv)
     WS<N> w = carve<N>(wsb + (size_t)wv * ws_doubles<N>(P.nc_max, P.ne_max, P.mr4), P.nc_max, P.ne_max, P.mr4);
     double gxg, gyg, uj;
     int legv;
-    prologue<N>(P, w, G, E, b, gxg, gyg, legv, uj);
+    prologue<N, true>(P, w, G, E, b, gxg, gyg, legv, uj);
     const int nc_sel = w.nsel[0], ne_sel = w.nsel[1];
     const double fk = state_pass<N, true>(P, w.V, w.CT, w.ST, w.gfg, gxg, gyg);
     const double f = wsum(fk);
@@ -1255,9 +1303,11 @@ using namespace alip;
 struct Handle {
     alipmpc_cfg cfg;
     int device = 0;
-    int N = 3, n = 15, NG = 32, NCP = 16, rps = 0, m_max = 0, mr4 = 0;
-    double* dG = nullptr;
-    double* dE = nullptr;
+    int N = 3, n = 9, NG = 32, NCP = 16, NCPU = 16, rps = 0, m_max = 0, mr4 = 0;
+    double* dGp = nullptr;
+    double* dEp = nullptr;
+    double* dGu = nullptr;
+    double* dEu = nullptr;
     // staging for host-pointer calls
     void* stage = nullptr;
     size_t stage_bytes = 0;
@@ -1289,10 +1339,15 @@ void mm(const double* a, const double* b, double* c, int n1, int n2, int n3)
         }
 }
 
-// generator tables: V = E x0 + G u, row 8k+c (c<5): x_k[c]; row 8k+5+c (c<3): p_k[c]
-void build_tables(const alipmpc_cfg& cfg, int NCP, std::vector<double>& G, std::vector<double>& E)
+// generator tables.  Row 8k+c (c<5): state x_k[c]; row 8k+5+c (c<3): foothold p_k[c]; V = E x0 + G z.
+//  u-parametrisation (the reference's decision, eval + warm start): x_{k+1} = M_A x_k + M_B u_k,
+//    p_k = W(u_k - A x_k)                                           (MPC_LIP_modi.py:64-87, 630-634)
+//  foothold parametrisation (the solve): x_{k+1} = A x_k + B p_k   (W B = I, so the two describe the same
+//    NLP; u enters it only through W u_k, which leaves a 2N-dim null space in u that p removes)
+void build_tables(const alipmpc_cfg& cfg, int NCPP, int NCPU, std::vector<double>& Gp, std::vector<double>& Ep,
+                  std::vector<double>& Gu, std::vector<double>& Eu)
 {
-    const int N = cfg.N, n = 5 * N, NG = 8 * (N + 1);
+    const int N = cfg.N, n = 5 * N, np_ = 3 * N, NG = 8 * (N + 1);
     const double b = std::sqrt(cfg.g / cfg.H), T = cfg.dt;
     const double ch = std::cosh(b * T), sh = std::sinh(b * T);
     double A[25] = {ch, 0, sh / b, 0, 0, 0, ch, 0, sh / b, 0, sh * b, 0, ch, 0, 0, 0, sh * b, 0, ch, 0, 0, 0, 0, 0, 1};
@@ -1306,35 +1361,55 @@ void build_tables(const alipmpc_cfg& cfg, int NCP, std::vector<double>& G, std::
     mm(MB, A, BWA, 5, 5, 5);
     for (int i = 0; i < 25; ++i) MA[i] = A[i] - BWA[i];
     mm(W, A, WA, 3, 5, 5);
+    // ---- u tables
     std::vector<double> Phi((N + 1) * 5 * n, 0.0), Pk((N + 1) * 25, 0.0);
-    for (int i = 0; i < 5; ++i) Pk[i * 5 + i] = 1.0;   // MA^0
+    for (int i = 0; i < 5; ++i) Pk[i * 5 + i] = 1.0;
     for (int k = 1; k <= N; ++k) {
         mm(MA, &Phi[(k - 1) * 5 * n], &Phi[k * 5 * n], 5, 5, n);
         for (int i = 0; i < 5; ++i)
             for (int j = 0; j < 5; ++j) Phi[k * 5 * n + i * n + 5 * (k - 1) + j] += MB[i * 5 + j];
         mm(MA, &Pk[(k - 1) * 25], &Pk[k * 25], 5, 5, 5);
     }
-    G.assign(NG * NCP, 0.0);
-    E.assign(NG * 5, 0.0);
+    Gu.assign((size_t)NG * NCPU, 0.0);
+    Eu.assign((size_t)NG * 5, 0.0);
     for (int k = 0; k <= N; ++k) {
         for (int c = 0; c < 5; ++c) {
-            for (int j = 0; j < n; ++j) G[(8 * k + c) * NCP + j] = Phi[k * 5 * n + c * n + j];
-            for (int j = 0; j < 5; ++j) E[(8 * k + c) * 5 + j] = Pk[k * 25 + c * 5 + j];
+            for (int j = 0; j < n; ++j) Gu[(8 * k + c) * NCPU + j] = Phi[k * 5 * n + c * n + j];
+            for (int j = 0; j < 5; ++j) Eu[(8 * k + c) * 5 + j] = Pk[k * 25 + c * 5 + j];
         }
         if (k < N) {
             std::vector<double> WAPhi(3 * n), WAPk(15);
             mm(WA, &Phi[k * 5 * n], WAPhi.data(), 3, 5, n);
             mm(WA, &Pk[k * 25], WAPk.data(), 3, 5, 5);
             for (int c = 0; c < 3; ++c) {
-                for (int j = 0; j < n; ++j) G[(8 * k + 5 + c) * NCP + j] = -WAPhi[c * n + j];
-                for (int j = 0; j < 5; ++j) G[(8 * k + 5 + c) * NCP + 5 * k + j] += W[c * 5 + j];
-                for (int j = 0; j < 5; ++j) E[(8 * k + 5 + c) * 5 + j] = -WAPk[c * 5 + j];
+                for (int j = 0; j < n; ++j) Gu[(8 * k + 5 + c) * NCPU + j] = -WAPhi[c * n + j];
+                for (int j = 0; j < 5; ++j) Gu[(8 * k + 5 + c) * NCPU + 5 * k + j] += W[c * 5 + j];
+                for (int j = 0; j < 5; ++j) Eu[(8 * k + 5 + c) * 5 + j] = -WAPk[c * 5 + j];
             }
         }
     }
+    // ---- foothold tables: x_k = A^k x0 + sum_{j<k} A^{k-1-j} B p_j
+    std::vector<double> Ak((N + 1) * 25, 0.0);
+    for (int i = 0; i < 5; ++i) Ak[i * 5 + i] = 1.0;
+    for (int k = 1; k <= N; ++k) mm(A, &Ak[(k - 1) * 25], &Ak[k * 25], 5, 5, 5);
+    Gp.assign((size_t)NG * NCPP, 0.0);
+    Ep.assign((size_t)NG * 5, 0.0);
+    for (int k = 0; k <= N; ++k) {
+        for (int c = 0; c < 5; ++c) {
+            for (int j = 0; j < 5; ++j) Ep[(8 * k + c) * 5 + j] = Ak[k * 25 + c * 5 + j];
+            for (int jj = 0; jj < k; ++jj) {
+                double AB[15];
+                mm(&Ak[(k - 1 - jj) * 25], Bm, AB, 5, 5, 3);
+                for (int c2 = 0; c2 < 3; ++c2) Gp[(8 * k + c) * NCPP + 3 * jj + c2] = AB[c * 3 + c2];
+            }
+        }
+        if (k < N)
+            for (int c = 0; c < 3; ++c) Gp[(8 * k + 5 + c) * NCPP + 3 * k + c] = 1.0;
+    }
+    (void)np_;
 }
 
-size_t smem_bytes(const Handle* h)
+size_t smem_bytes(const Handle* h, bool solve)
 {
     int wsd = 0;
     switch (h->N) {
@@ -1344,10 +1419,11 @@ size_t smem_bytes(const Handle* h)
 #undef WSCASE
     }
     const int e = h->NG * 5 + ((h->NG * 5) & 1);
-    return sizeof(double) * ((size_t)KP_DOUBLES + (size_t)h->NG * h->NCP + e + (size_t)WAVES_PER_BLOCK * wsd);
+    const int ncp = solve ? h->NCP : h->NCPU;
+    return sizeof(double) * ((size_t)KP_DOUBLES + (size_t)h->NG * ncp + e + (size_t)WAVES_PER_BLOCK * wsd);
 }
 
-KP make_kp(const Handle* h, long long B)
+KP make_kp(const Handle* h, long long B, bool solve)
 {
     const alipmpc_cfg& c = h->cfg;
     KP P;
@@ -1376,8 +1452,10 @@ KP make_kp(const Handle* h, long long B)
     P.bvy_hi = c.bvy_hi;
     P.dth = c.dtheta_max;
     P.mu_init = c.mu_init;
-    P.G = h->dG;
-    P.E = h->dE;
+    P.G = solve ? h->dGp : h->dGu;
+    P.E = solve ? h->dEp : h->dEu;
+    P.Gu = h->dGu;
+    P.Eu = h->dEu;
     P.B = B;
     return P;
 }
@@ -1403,7 +1481,7 @@ hipError_t launch_t(bool solve, const KP& P, size_t smem, hipStream_t st)
 
 hipError_t launch(const Handle* h, bool solve, const KP& P, hipStream_t st)
 {
-    const size_t smem = smem_bytes(h);
+    const size_t smem = smem_bytes(h, solve);
     switch (h->N) {
     case 1: return launch_t<1>(solve, P, smem, st);
     case 2: return launch_t<2>(solve, P, smem, st);
@@ -1521,9 +1599,10 @@ int alipmpc_create(const alipmpc_cfg* cfg, int device, void** handle)
     h->cfg = *cfg;
     h->device = device;
     h->N = cfg->N;
-    h->n = 5 * cfg->N;
+    h->n = 3 * cfg->N;
     h->NG = 8 * (cfg->N + 1);
     h->NCP = 16 * ((h->n + 15) / 16);
+    h->NCPU = 16 * ((5 * cfg->N + 15) / 16);
     h->rps = alipmpc_rows_per_step(cfg);
     h->m_max = cfg->N * h->rps;
     h->mr4 = (h->m_max + 3) & ~3;
@@ -1535,18 +1614,19 @@ int alipmpc_create(const alipmpc_cfg* cfg, int device, void** handle)
         delete h;
         return ALIPMPC_ENODEV;
     }
-    std::vector<double> G, E;
-    build_tables(*cfg, h->NCP, G, E);
-    if (hipMalloc(&h->dG, G.size() * sizeof(double)) != hipSuccess ||
-        hipMalloc(&h->dE, E.size() * sizeof(double)) != hipSuccess ||
-        hipMemcpy(h->dG, G.data(), G.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(h->dE, E.data(), E.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
+    std::vector<double> Gp, Ep, Gu, Eu;
+    build_tables(*cfg, h->NCP, h->NCPU, Gp, Ep, Gu, Eu);
+    auto up = [](double** d, const std::vector<double>& v) {
+        return hipMalloc(d, v.size() * sizeof(double)) == hipSuccess &&
+               hipMemcpy(*d, v.data(), v.size() * sizeof(double), hipMemcpyHostToDevice) == hipSuccess;
+    };
+    if (!up(&h->dGp, Gp) || !up(&h->dEp, Ep) || !up(&h->dGu, Gu) || !up(&h->dEu, Eu) ||
         hipStreamCreateWithFlags(&h->own, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess) {
         alipmpc_destroy(h);
         return ALIPMPC_EHIP;
     }
-    if (smem_bytes(h) > 160 * 1024) {
+    if (smem_bytes(h, true) > 160 * 1024 || smem_bytes(h, false) > 160 * 1024) {
         alipmpc_destroy(h);
         return ALIPMPC_EUNSUPPORTED;
     }
@@ -1568,9 +1648,9 @@ static int run_batch(Handle* h, bool solve, int64_t B, const double* x0, const d
     if (solve && !u_out) return fail(h, ALIPMPC_EINVAL, "u_out is required");
     HIPCHK(h, hipSetDevice(h->device));
     const alipmpc_cfg& cf = h->cfg;
-    const int n = h->n, N = h->N;
+    const int n = 5 * h->N, N = h->N;     // host-facing u is the reference's 5N-vector
     const size_t mm_ = (size_t)h->m_max;
-    KP P = make_kp(h, B);
+    KP P = make_kp(h, B, solve);
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : h->own;
     if (hip_stream) {
         P.x0 = x0; P.goal = goal; P.leg = leg; P.cir = cir; P.nc = nc; P.elp = elp; P.ne = ne; P.u0 = u0;
@@ -1705,8 +1785,8 @@ void alipmpc_destroy(void* handle)
     if (!h) return;
     hipSetDevice(h->device);
     if (h->own) hipStreamSynchronize(h->own);
-    if (h->dG) hipFree(h->dG);
-    if (h->dE) hipFree(h->dE);
+    for (double* d : {h->dGp, h->dEp, h->dGu, h->dEu})
+        if (d) (void)hipFree(d);
     if (h->stage) hipFree(h->stage);
     if (h->ev0) hipEventDestroy(h->ev0);
     if (h->ev1) hipEventDestroy(h->ev1);

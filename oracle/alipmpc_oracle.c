@@ -36,6 +36,9 @@ typedef struct {
     double A[5][5], B[5][3], W[3][5], MA[5][5], MB[5][5];
     double Phi[OMAXN + 1][5][OMAXV]; /* d x_k / du */
     double Psi[OMAXN][3][OMAXV];     /* d p_k / du */
+    /* foothold parametrisation (W B = I): u(p) = [A^k x0]_k + U p, U block lower-triangular A^{k-1-j} B */
+    double Ak[OMAXN + 1][5][5];
+    double U[OMAXV][3 * OMAXN];
 } oconsts;
 
 typedef struct {
@@ -149,6 +152,16 @@ void oracle_consts(const alipmpc_cfg* cfg, oconsts* K)
         for (int i = 0; i < 5; ++i)
             for (int j = 0; j < 5; ++j) K->Phi[k][i][5 * (k - 1) + j] += K->MB[i][j];
     }
+    for (int i = 0; i < 5; ++i) K->Ak[0][i][i] = 1.0;
+    for (int k = 1; k <= cfg->N; ++k) mm55(K->A, K->Ak[k - 1], K->Ak[k]);
+    for (int k = 1; k <= cfg->N; ++k)
+        for (int j = 0; j < k; ++j)
+            for (int a = 0; a < 5; ++a)
+                for (int c = 0; c < 3; ++c) {
+                    double acc = 0;
+                    for (int t = 0; t < 5; ++t) acc += K->Ak[k - 1 - j][a][t] * K->B[t][c];
+                    K->U[5 * (k - 1) + a][3 * j + c] = acc;
+                }
     for (int k = 0; k < cfg->N; ++k) {
         double WA[3][5];
         for (int i = 0; i < 3; ++i)
@@ -604,11 +617,87 @@ typedef struct {
     int iters, status, restorations;
 } osolve_info;
 
+/* foothold-space views of the NLP: u(p) = [A^k x0]_k + U p  (the solve runs on p, n = 3N) */
+static void u_of_p(const oprob* P, const double* pv, double* u)
+{
+    const oconsts* K = P->K;
+    const int N = P->N, np_ = 3 * N;
+    for (int k = 1; k <= N; ++k)
+        for (int a = 0; a < 5; ++a) {
+            double acc = 0;
+            for (int t = 0; t < 5; ++t) acc += K->Ak[k][a][t] * P->x0[t];
+            for (int j = 0; j < np_; ++j) acc += K->U[5 * (k - 1) + a][j] * pv[j];
+            u[5 * (k - 1) + a] = acc;
+        }
+}
+static double pobj(const oprob* P, const double* pv)
+{
+    double u[OMAXV];
+    u_of_p(P, pv, u);
+    return oracle_objective(P, u);
+}
+static void pcons(const oprob* P, const double* pv, double* c)
+{
+    double u[OMAXV];
+    u_of_p(P, pv, u);
+    constraints(P, u, c);
+}
+static void pgrad(const oprob* P, const double* pv, double* gp)
+{
+    double u[OMAXV], gu[OMAXV];
+    u_of_p(P, pv, u);
+    gradient(P, u, gu);
+    const int nu = 5 * P->N, np_ = 3 * P->N;
+    for (int j = 0; j < np_; ++j) {
+        double acc = 0;
+        for (int i = 0; i < nu; ++i) acc += P->K->U[i][j] * gu[i];
+        gp[j] = acc;
+    }
+}
+static void pjac(const oprob* P, const double* pv, double* Jp)
+{
+    static __thread double Ju[OMAXM * OMAXV];
+    double u[OMAXV];
+    u_of_p(P, pv, u);
+    jacobian(P, u, Ju);
+    const int nu = 5 * P->N, np_ = 3 * P->N;
+    for (int r = 0; r < P->m; ++r)
+        for (int j = 0; j < np_; ++j) {
+            double acc = 0;
+            for (int i = 0; i < nu; ++i) acc += Ju[r * nu + i] * P->K->U[i][j];
+            Jp[r * np_ + j] = acc;
+        }
+}
+static void phess(const oprob* P, const double* pv, const double* y, double* Hp)
+{
+    double u[OMAXV], Hu[OMAXV * OMAXV], T[OMAXV * 3 * OMAXN];
+    u_of_p(P, pv, u);
+    hessian(P, u, y, Hu);
+    const int nu = 5 * P->N, np_ = 3 * P->N;
+    for (int i = 0; i < nu; ++i)
+        for (int j = 0; j < np_; ++j) {
+            double acc = 0;
+            for (int t = 0; t < nu; ++t) acc += Hu[i * nu + t] * P->K->U[t][j];
+            T[i * np_ + j] = acc;
+        }
+    for (int a = 0; a < np_; ++a)
+        for (int b = 0; b < np_; ++b) {
+            double acc = 0;
+            for (int i = 0; i < nu; ++i) acc += P->K->U[i][a] * T[i * np_ + b];
+            Hp[a * np_ + b] = acc;
+        }
+}
+
+#define REST_FAIL 6
+
+
+
 /* Primal-dual interior point with IPOPT's filter line search; mirrors np_oracle.solve. */
-static void osolve(oprob* P, const double* u0, double* u, osolve_info* info)
+static void osolve(oprob* P, const double* u0, double* uout, osolve_info* info)
 {
     const alipmpc_cfg* cfg = P->cfg;
-    const int n = P->n, m = P->m;
+    const int n = 3 * P->N, m = P->m;
+    double u[OMAXV];   /* the decision: footholds p (n = 3N) */
     const int smooth = P->modi;
     double cl[OMAXM], cu[OMAXM];
     int hl[OMAXM], hu[OMAXM];
@@ -620,11 +709,16 @@ static void osolve(oprob* P, const double* u0, double* u, osolve_info* info)
         cl[i] = hl[i] ? P->cl[i] - 1e-8 * fmax(1.0, fabs(P->cl[i])) : -INFINITY;
         cu[i] = hu[i] ? P->cu[i] + 1e-8 * fmax(1.0, fabs(P->cu[i])) : INFINITY;
     }
-    memcpy(u, u0, n * sizeof(double));
+    {
+        double X0[OMAXN + 1][5], Pp0[OMAXN][3];
+        rollout(P, u0, X0, Pp0);
+        for (int k = 0; k < P->N; ++k)
+            for (int c = 0; c < 3; ++c) u[3 * k + c] = Pp0[k][c];
+    }
     double mu = cfg->mu_init;
     P->eps_abs = smooth ? eps_abs_of_mu(mu) : 0.0;
     double c[OMAXM], s[OMAXM], zl[OMAXM], zu[OMAXM];
-    constraints(P, u, c);
+    pcons(P, u, c);
     push_slacks(c, cl, cu, m, s);
     for (int i = 0; i < m; ++i) {
         zl[i] = hl[i] ? 1.0 : 0.0;
@@ -644,9 +738,9 @@ static void osolve(oprob* P, const double* u0, double* u, osolve_info* info)
     double dl[OMAXM], du[OMAXM], rc[OMAXM], Sig[OMAXM], dU[OMAXV], dS[OMAXM], dZl[OMAXM], dZu[OMAXM];
     double ut[OMAXV], st[OMAXM], ct[OMAXM];
     for (it = 0; it <= cfg->max_iter; ++it) {
-        double f = oracle_objective(P, u);
-        gradient(P, u, gf);
-        jacobian(P, u, J);
+        double f = pobj(P, u);
+        pgrad(P, u, gf);
+        pjac(P, u, J);
         double nz = 0;
         for (int i = 0; i < m; ++i) {
             dl[i] = hl[i] ? s[i] - cl[i] : 1.0;
@@ -691,16 +785,16 @@ static void osolve(oprob* P, const double* u0, double* u, osolve_info* info)
             nf = 0;
             if (smooth) {
                 P->eps_abs = eps_abs_of_mu(mu);
-                f = oracle_objective(P, u);
-                gradient(P, u, gf);
-                jacobian(P, u, J);
-                constraints(P, u, c);
+                f = pobj(P, u);
+                pgrad(P, u, gf);
+                pjac(P, u, J);
+                pcons(P, u, c);
                 for (int i = 0; i < m; ++i) rc[i] = c[i] - s[i];
             }
         }
         double tau = fmax(0.99, 1.0 - mu);
         for (int i = 0; i < m; ++i) Sig[i] = (hl[i] ? zl[i] / dl[i] : 0.0) + (hu[i] ? zu[i] / du[i] : 0.0);
-        hessian(P, u, y, H);
+        phess(P, u, y, H);
         for (int a = 0; a < n; ++a) {
             for (int b = 0; b < n; ++b) {
                 double acc = 0;
@@ -769,8 +863,8 @@ static void osolve(oprob* P, const double* u0, double* u, osolve_info* info)
         while (a >= amin) {
             for (int j = 0; j < n; ++j) ut[j] = u[j] + a * dU[j];
             for (int i = 0; i < m; ++i) st[i] = s[i] + a * dS[i];
-            constraints(P, ut, ct);
-            double ftv = oracle_objective(P, ut);
+            pcons(P, ut, ct);
+            double ftv = pobj(P, ut);
             double tht = 0;
             for (int i = 0; i < m; ++i) tht += fabs(ct[i] - st[i]);
             double pht = barrier(ftv, st, cl, cu, m, mu);
@@ -805,9 +899,19 @@ static void osolve(oprob* P, const double* u0, double* u, osolve_info* info)
             n_rest++;
             a = fmax(a, amin);
             for (int j = 0; j < n; ++j) u[j] += a * dU[j];
-            constraints(P, u, c);
+            pcons(P, u, c);
             push_slacks(c, cl, cu, m, s);
             nf = 0;
+            double viol = 0;
+            for (int i = 0; i < m; ++i) {
+                if (hl[i]) viol = fmax(viol, P->cl[i] - c[i]);
+                if (hu[i]) viol = fmax(viol, c[i] - P->cu[i]);
+            }
+            if (n_rest >= REST_FAIL && viol > 1e-4) {
+                status = 2;
+                it++;
+                break;
+            }
         }
         for (int i = 0; i < m; ++i) {
             zl[i] += az * dZl[i];
@@ -827,8 +931,8 @@ static void osolve(oprob* P, const double* u0, double* u, osolve_info* info)
     }
     free(ft);
     P->eps_abs = 0.0;
-    if (status != 0) {
-        constraints(P, u, c);
+    if (status != 0 && status != 2) {
+        pcons(P, u, c);
         double viol = 0;
         for (int i = 0; i < m; ++i) {
             if (hl[i]) viol = fmax(viol, P->cl[i] - c[i]);
@@ -839,6 +943,7 @@ static void osolve(oprob* P, const double* u0, double* u, osolve_info* info)
         else if (viol > 1e-4)
             status = 2;
     }
+    u_of_p(P, u, uout);
     info->iters = it;
     info->status = status;
     info->restorations = n_rest;

@@ -76,7 +76,7 @@ def _batch_inputs(cfg, x0, goal, leg, cir, nc, elp, ne):
     leg = np.ascontiguousarray(leg, np.int8).reshape(B)
     cir = np.ascontiguousarray(cir, np.float64).reshape(B, cfg.nc_max, 3)
     nc = np.ascontiguousarray(nc, np.int32).reshape(B)
-    if cfg.ne_max > 0:
+    if cfg.ne_max > 0 and elp is not None:
         elp = np.ascontiguousarray(elp, np.float64).reshape(B, cfg.ne_max, 5)
         ne = np.ascontiguousarray(ne, np.int32).reshape(B)
     else:

@@ -1,0 +1,230 @@
+"""GPU parity tests: the HIP kernels behind libalipmpc.so, called through the C ABI, against the reference
+goldens (tests/golden) and the oracle (oracle/) on the same seeded inputs."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REL = 1e-12
+
+
+def rel(a, b):
+    a, b = np.asarray(a, float), np.asarray(b, float)
+    return float(np.max(np.abs(a - b) / (1.0 + np.abs(b)))) if a.size else 0.0
+
+
+def _oracle_solve(coracle, cfg_kw, bt, nthreads=8):
+    cfg = coracle.default_cfg(**cfg_kw)
+    return coracle.solve_batch(cfg, bt["x0"], bt["goal"], bt["leg"], bt["cir"], bt["nc"], bt.get("elp"),
+                               bt.get("ne"), bt["u0"], nthreads=nthreads)
+
+
+def _compare(out, ref, min_conv=0.8, min_agree=0.97, min_status=0.97):
+    """Parity on the foothold p_list[0] and the predicted states where both solves converged (the NLP is
+    nonconvex: rounding-level differences can steer a few instances into another basin)."""
+    both = (out["status"] == 0) & (ref["status"] == 0)
+    assert both.mean() >= min_conv, both.mean()
+    scale = np.maximum(1.0, np.abs(ref["foot"]))
+    ok = np.all(np.abs(out["foot"] - ref["foot"]) <= 1e-4 * scale, axis=1)
+    okx = np.all(np.abs(out["x_pred"] - ref["x_pred"]).reshape(len(ok), -1) <= 1e-4 * np.maximum(1.0, np.abs(ref["x_pred"]).reshape(len(ok), -1)), axis=1)
+    agree = (ok & okx)[both].mean()
+    assert agree >= min_agree, agree
+    same_status = (out["status"] == ref["status"]).mean()
+    assert same_status >= min_status, same_status
+    return agree
+
+
+@pytest.mark.parametrize("name,variant", [("modi", 0), ("sig_step", 1)])
+def test_eval_matches_reference_callbacks(gpu_lib, golden, name, variant):
+    g = golden(f"g1_callbacks_{name}")
+    cfg = gpu_lib.default_cfg(variant, select_obs=0, detour=0)
+    s = gpu_lib.Solver(cfg)
+    B = len(g["f"])
+    o = s.eval(g["x0"], g["goal"], np.ones(B), g["cir"], g["nc"], g["elp"], g["ne"], g["u"])
+    assert rel(o["f"], g["f"]) < REL
+    assert rel(o["grad"], g["grad"]) < REL
+    for t in range(B):
+        act = o["row_active"][t].astype(bool)
+        m = g["m"][t]
+        assert act.sum() == m
+        assert rel(o["c"][t][act], g["c"][t][:m]) < REL
+        assert rel(o["J"][t][act], g["J"][t][:m]) < REL
+        assert np.all(o["c"][t][~act] == 0) and np.all(o["J"][t][~act] == 0)
+
+
+def test_eval_horizon5(gpu_lib, golden, coracle):
+    g = golden("g1_callbacks_modi_n5")
+    B = len(g["f"])
+    cfg = gpu_lib.default_cfg(0, 5, nc_max=10, ne_max=10, select_obs=0, detour=0)
+    s = gpu_lib.Solver(cfg)
+    o = s.eval(g["x0"], g["goal"], np.ones(B), g["cir"], g["nc"], g["elp"], g["ne"], g["u"])
+    assert rel(o["f"], g["f"]) < REL
+    cc = coracle.default_cfg(0, 5, nc_max=10, ne_max=10, select_obs=0, detour=0)
+    r = coracle.eval_batch(cc, g["x0"], g["goal"], np.ones(B), g["cir"], g["nc"], g["elp"], g["ne"], g["u"])
+    assert rel(o["grad"], r["grad"]) < REL
+    assert rel(o["J"], r["J"]) < REL
+    for t in range(B):
+        act = o["row_active"][t].astype(bool)
+        assert rel(o["c"][t][act], g["c"][t][:g["m"][t]]) < REL
+
+
+@pytest.mark.parametrize("name,variant", [("modi", 0), ("sig_step", 1)])
+def test_setup_matches_reference(gpu_lib, golden, name, variant):
+    g = golden(f"g2_setup_{name}")
+    B = len(g["m"])
+    cfg = gpu_lib.default_cfg(variant)
+    s = gpu_lib.Solver(cfg)
+    o = s.eval(g["x0"], g["goal"], g["leg"], g["cir"], g["nc"], g["elp"], g["ne"], np.tile(g["x0"], (1, 3)))
+    for t in range(B):
+        act = o["row_active"][t].astype(bool)
+        m = g["m"][t]
+        assert act.sum() == m
+        assert np.array_equal(o["cl"][t][act], g["cl"][t][:m])
+        assert np.array_equal(o["cu"][t][act], g["cu"][t][:m])
+        assert np.allclose(o["goal_eff"][t], g["goal_eff"][t], rtol=0, atol=1e-14)
+        assert np.all(np.isneginf(o["cl"][t][~act])) and np.all(np.isposinf(o["cu"][t][~act]))
+
+
+def test_solve_sup_learn_recorded_cyipopt(gpu_lib, golden, coracle):
+    d = golden("g3_sup_learn")
+    B = len(d["leg"])
+    cfg = gpu_lib.default_cfg(0, nc_max=6, ne_max=0)
+    s = gpu_lib.Solver(cfg)
+    cir = np.tile(d["cir_safe"], (B, 1, 1))
+    o = s.solve(d["x_nex"], [10, 10], d["leg"], cir, np.full(B, 6), u0=d["u0"])
+    ok = d["ok_ref"].astype(bool)
+    err = np.max(np.abs(o["foot"][:, :2] - d["foot_logged"]), axis=1)
+    assert (err[ok] < 1e-4).sum() >= int(0.97 * ok.sum())
+    bt = dict(x0=d["x_nex"], goal=np.tile([10.0, 10.0], (B, 1)), leg=d["leg"], cir=cir, nc=np.full(B, 6),
+              u0=d["u0"])
+    ref = _oracle_solve(coracle, dict(variant=0, nc_max=6, ne_max=0), bt)
+    _compare(o, ref)
+
+
+@pytest.mark.parametrize("variant,name", [(0, "modi"), (1, "sig_step")])
+def test_solve_synthetic_scipy_goldens(gpu_lib, golden, variant, name):
+    d = golden(f"g3_synthetic_{name}")
+    good = (d["agree"] < 1e-8) & (d["viol"] < 1e-8)
+    cfg = gpu_lib.default_cfg(variant, nc_max=6, ne_max=6)
+    s = gpu_lib.Solver(cfg)
+    o = s.solve(d["x0"], d["goal"], d["leg"], d["cir"], d["nc"], d["elp"], d["ne"], u0=d["u0"])
+    err = np.max(np.abs(o["foot"] - d["foot_ref"]), axis=1)
+    assert np.all(err[good] < 1e-4), err[good].max()
+
+
+def test_solve_cfg2_batch_vs_oracle(gpu_lib, coracle):
+    from alipmpc import scenes
+    bt = scenes.make_batch(2048, seed=11, n_cir=5)
+    s = gpu_lib.Solver(gpu_lib.default_cfg(0, nc_max=5, ne_max=0))
+    o = s.solve(bt["x0"], bt["goal"], bt["leg"], bt["cir"], bt["nc"], u0=bt["u0"])
+    ref = _oracle_solve(coracle, dict(variant=0, nc_max=5, ne_max=0), bt)
+    _compare(o, ref)
+    # u is the canonical u_k = x_{k+1}; foot and states are consistent with the ALIP step map
+    assert np.allclose(o["u"].reshape(-1, 3, 5), o["x_pred"], rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("variant,N,n_cir,n_elp", [(1, 3, 4, 0), (0, 3, 3, 3), (0, 5, 5, 5), (0, 1, 2, 0),
+                                                   (0, 4, 5, 0), (0, 6, 3, 0)])
+def test_solve_variants_vs_oracle(gpu_lib, coracle, variant, N, n_cir, n_elp):
+    from alipmpc import scenes
+    bt = scenes.make_batch(256, seed=100 + N + n_elp, n_cir=n_cir, n_elp=n_elp, N=N)
+    cfg = gpu_lib.default_cfg(variant, N, nc_max=n_cir, ne_max=n_elp)
+    s = gpu_lib.Solver(cfg)
+    o = s.solve(bt["x0"], bt["goal"], bt["leg"], bt["cir"], bt["nc"], bt["elp"], bt["ne"], u0=bt["u0"])
+    ref = _oracle_solve(coracle, dict(variant=variant, N=N, nc_max=n_cir, ne_max=n_elp), bt)
+    _compare(o, ref, min_conv=0.5, min_agree=0.95, min_status=0.9)
+
+
+def test_edge_cases(gpu_lib, coracle):
+    from alipmpc import scenes
+    s = gpu_lib.Solver(gpu_lib.default_cfg(0, nc_max=5, ne_max=0))
+    bt = scenes.make_batch(8, seed=3, n_cir=5)
+    # empty batch is a no-op
+    o = s.solve(bt["x0"][:0], bt["goal"][:0], bt["leg"][:0], bt["cir"][:0], bt["nc"][:0], u0=bt["u0"][:0])
+    assert o["u"].shape == (0, 15)
+    # ragged obstacle counts, including none, and obstacles all outside the 4 m detection range
+    nc = np.array([0, 1, 2, 3, 4, 5, 5, 5], np.int32)
+    cir = bt["cir"].copy()
+    cir[6, :, :2] += 50.0
+    o = s.solve(bt["x0"], bt["goal"], bt["leg"], cir, nc, u0=bt["u0"])
+    ref = coracle.solve_batch(coracle.default_cfg(0, nc_max=5, ne_max=0), bt["x0"], bt["goal"], bt["leg"], cir, nc,
+                              None, None, bt["u0"])
+    both = (o["status"] == 0) & (ref["status"] == 0)
+    assert both.sum() >= 6
+    assert np.all(np.abs(o["foot"] - ref["foot"])[both] <= 1e-4 * np.maximum(1.0, np.abs(ref["foot"][both])))
+    # B = 1
+    o1 = s.solve(bt["x0"][:1], bt["goal"][:1], bt["leg"][:1], cir[:1], nc[:1], u0=bt["u0"][:1])
+    assert np.array_equal(o1["foot"][0], o["foot"][0])
+    # a CoM velocity the step-to-step model cannot bring into the body-velocity bounds with a leg of at
+    # most 0.3 m is infeasible: status 2 (the reference's "fail"), the iterate is still returned
+    x0 = bt["x0"][:1].copy()
+    x0[0, 2:4] = [3.0, 3.0]
+    o2 = s.solve(x0, bt["goal"][:1], bt["leg"][:1], cir[:1], nc[:1], u0=np.tile(x0, (1, 3)))
+    assert o2["status"][0] == 2 and np.all(np.isfinite(o2["u"]))
+    # max slot counts: 8 circles + 8 ellipses (m = 3 * 21 rows)
+    bt16 = scenes.make_batch(64, seed=5, n_cir=8, n_elp=8)
+    s16 = gpu_lib.Solver(gpu_lib.default_cfg(0, nc_max=8, ne_max=8))
+    o16 = s16.solve(bt16["x0"], bt16["goal"], bt16["leg"], bt16["cir"], bt16["nc"], bt16["elp"], bt16["ne"],
+                    u0=bt16["u0"])
+    ref16 = _oracle_solve(coracle, dict(variant=0, nc_max=8, ne_max=8), bt16)
+    _compare(o16, ref16, min_conv=0.5, min_agree=0.9, min_status=0.9)
+
+
+def test_invalid_arguments_raise(gpu_lib):
+    with pytest.raises(RuntimeError):
+        gpu_lib.Solver(gpu_lib.default_cfg(0, 7))            # horizon above the kernel limit
+    with pytest.raises(RuntimeError):
+        gpu_lib.Solver(gpu_lib.default_cfg(0, 3, nc_max=20, ne_max=20))
+
+
+def test_device_pointer_mode_and_determinism(gpu_lib):
+    import torch
+    from alipmpc import scenes
+    B = 1024
+    bt = scenes.make_batch(B, seed=21, n_cir=5)
+    s = gpu_lib.Solver(gpu_lib.default_cfg(0, nc_max=5, ne_max=0))
+    host = s.solve(bt["x0"], bt["goal"], bt["leg"], bt["cir"], bt["nc"], u0=bt["u0"])
+    dev = torch.device("cuda", 0)
+    inp = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in bt.items() if v is not None}
+    inp["leg"] = inp["leg"].to(torch.int8)
+    inp["nc"] = inp["nc"].to(torch.int32)
+    out = {"u": torch.empty((B, 15), dtype=torch.float64, device=dev),
+           "foot": torch.empty((B, 3), dtype=torch.float64, device=dev),
+           "x_pred": torch.empty((B, 3, 5), dtype=torch.float64, device=dev),
+           "status": torch.empty(B, dtype=torch.int32, device=dev),
+           "iters": torch.empty(B, dtype=torch.int32, device=dev)}
+    s.solve_device(inp, out)
+    torch.cuda.synchronize()
+    assert np.array_equal(out["foot"].cpu().numpy(), host["foot"])
+    assert np.array_equal(out["status"].cpu().numpy(), host["status"])
+    host2 = s.solve(bt["x0"], bt["goal"], bt["leg"], bt["cir"], bt["nc"], u0=bt["u0"])
+    assert np.array_equal(host2["u"], host["u"]) and np.array_equal(host2["iters"], host["iters"])
+
+
+def test_full_size_properties_cfg3(gpu_lib):
+    """BASELINE configs[2] size (B = 65536, N = 5, 5 circles + 5 ellipses): size-independent properties of
+    every returned plan — finite outputs, valid statuses, the ALIP step map between foot, u and states,
+    and, for converged instances, feasibility of the reference constraints at the returned u (evaluated by
+    the eval kernel) within the solver tolerance."""
+    from alipmpc import scenes
+    B = 65536
+    bt = scenes.make_batch(B, seed=33, n_cir=5, n_elp=5, N=5, scenes_per_batch=512)
+    cfg = gpu_lib.default_cfg(0, 5, nc_max=5, ne_max=5)
+    s = gpu_lib.Solver(cfg)
+    o = s.solve(bt["x0"], bt["goal"], bt["leg"], bt["cir"], bt["nc"], bt["elp"], bt["ne"], u0=bt["u0"])
+    assert np.all(np.isfinite(o["u"])) and np.all(np.isfinite(o["foot"]))
+    assert set(np.unique(o["status"]).tolist()) <= {-1, 0, 1, 2}
+    assert (o["status"] == 0).mean() > 0.7
+    assert np.array_equal(o["u"].reshape(B, 5, 5), o["x_pred"])
+    ev = s.eval(bt["x0"], bt["goal"], bt["leg"], bt["cir"], bt["nc"], bt["elp"], bt["ne"], o["u"], want_J=False)
+    conv = o["status"] == 0
+    act = ev["row_active"].astype(bool)
+    viol = np.maximum(ev["cl"] - ev["c"], ev["c"] - ev["cu"])
+    viol[~act] = 0
+    assert np.max(viol[conv]) < 1e-6
+    # foot = p_0 = W (u_1 - A x0) is exactly the step map the eval kernel sees: x_1 = A x0 + B p_0
+    import alipmpc.planner as pl
+    beta = np.sqrt(9.81)
+    A, Bm = pl._alip_matrices(beta, 0.4, 0.4)
+    x1 = bt["x0"] @ A.T + o["foot"] @ Bm.T
+    assert np.max(np.abs(x1 - o["x_pred"][:, 0])) < 1e-12

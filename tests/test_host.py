@@ -1,0 +1,136 @@
+"""CPU: host-side pieces — the C ABI library exports, the reference-facing planner helpers, the synthetic
+scene generator, and the multi-rank sharding/gather logic (gloo, world size 2)."""
+import os
+import re
+import ctypes
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "alipmpc.h")).read()
+    return sorted(set(re.findall(r"\b(alipmpc_[a-z_]+)\s*\(", src)))
+
+
+def test_library_builds_and_exports_every_header_symbol():
+    import alipmpc
+    from alipmpc import build
+    build.build()                                  # hipcc cross-compiles gfx950 without a GPU
+    lib = ctypes.CDLL(build.LIB)
+    declared = header_functions()
+    assert set(declared) == set(alipmpc.EXPORTS)
+    for sym in declared:
+        assert hasattr(lib, sym), sym
+
+
+def test_default_cfg_matches_reference_constants():
+    import alipmpc
+    c = alipmpc.default_cfg(alipmpc.VARIANT_MODI, 3)
+    # MPC_LIP_modi.py:35-41, 397-411
+    assert (c.leg2_max, c.bvx_lo, c.bvx_hi, c.bvy_lo, c.bvy_hi) == (0.09, 0.4, 0.8, 0.15, 0.35)
+    assert (c.p, c.q, c.r, c.gamma) == (0.0, 1.0, 50.0, 0.2)
+    assert abs(c.s - 0.024 * 180 / np.pi) < 1e-15 and abs(c.dtheta_max - np.pi / 16) < 1e-15
+    s = alipmpc.default_cfg(alipmpc.VARIANT_SIG_STEP, 3)
+    # MPC_LIP_sig_step.py:38, 340-353
+    assert (s.bvy_hi, s.p, s.q, s.r, s.gamma, s.select_obs) == (0.30, 2.0, 1.0, 15.0, 0.4, 0)
+    assert alipmpc.rows_per_step(c) == 4 + 6 + 6 + 1 and alipmpc.rows_per_step(s) == 4 + 6 + 6
+    assert alipmpc.num_vars(c) == 15
+
+
+def test_no_device_fails_loudly():
+    import torch
+    import alipmpc
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    with pytest.raises(RuntimeError, match="ENODEV"):
+        alipmpc.Solver(alipmpc.default_cfg(0, 3))
+
+
+def test_planner_host_helpers_match_reference(golden):
+    from alipmpc import planner
+    g = golden("g4_aux")
+    beta = np.sqrt(9.81)
+    for row, out, trk, ln in zip(g["gns_in"], g["gns_out"], g["trk"], g["trk_len"]):
+        xn, det = planner.next_state(beta, 0.4, row[0:2], row[2:4], row[4], row[5:8], row[8])
+        assert np.max(np.abs(xn - out)) < 1e-13
+        assert det.shape == (ln, 2) and np.max(np.abs(det - trk[:ln])) < 1e-12
+    obj = planner._Base.__new__(planner._Base)
+    obj.beta, obj.dt, obj.step_gap = beta, 0.4, 0.3
+    obj.sigma = beta / np.tanh(0.4 * beta / 2)
+    assert abs(obj.sigma - g["sigma"]) < 1e-12
+    for vx, leg, ex, ey in g["alip_des_vel"]:
+        assert np.allclose(obj.alip_des_vel(vx, leg), [ex, ey], rtol=0, atol=1e-14)
+    A, B = planner._alip_matrices(beta, 0.4, 0.4)
+    obj.A = A
+    obj.inv_B_vel_shr = np.linalg.inv(B[2:4, 0:2])
+    for inp, out in zip(g["cfv_in"], g["cfv_out"]):
+        assert np.allclose(obj.cal_foot_with_veldes(inp[:5], inp[5:]), out, rtol=0, atol=1e-12)
+    for h, v0, out in zip(g["tube_in"], g["tube_init"], g["tube_out"]):
+        assert np.allclose(obj.tube_func(h, v0), out, rtol=0, atol=1e-15)
+
+
+def test_sup_learn_state_projection_is_bit_exact(golden):
+    """get_next_states reproduces the logged x_nex of every recorded MPC call exactly."""
+    d = golden("g3_sup_learn")
+    assert np.max(np.abs(d["x_nex"][:, :2] - d["x_nex_logged"])) == 0.0
+
+
+def test_scene_generator_distribution():
+    from alipmpc import scenes
+    bt = scenes.make_batch(200, seed=1, n_cir=5)
+    assert bt["cir"].shape == (200, 5, 3) and np.all(bt["nc"] == 5)
+    r = bt["cir"][:, :, 2] - scenes.SAFE_DIS
+    assert r.min() >= 0.35 - 1e-12 and r.max() <= 1.0 + 1e-12
+    assert bt["cir"][:, :, :2].min() >= 0 and bt["cir"][:, :, :2].max() <= 8.5
+    for b in range(200):
+        c = bt["cir"][b]
+        d = np.hypot(*(bt["x0"][b, :2] - c[:, :2]).T)
+        assert np.all(d >= c[:, 2] + 0.2 - 1e-12)
+        for i in range(5):
+            for j in range(i):
+                ri, rj = c[i, 2] - 0.4, c[j, 2] - 0.4
+                assert np.hypot(*(c[i, :2] - c[j, :2])) >= ri + rj + 1.6 - 1e-9
+    vb = np.cos(bt["x0"][:, 4]) * bt["x0"][:, 2] + np.sin(bt["x0"][:, 4]) * bt["x0"][:, 3]
+    assert vb.min() >= 0.45 - 1e-12 and vb.max() <= 0.75 + 1e-12
+    assert np.array_equal(bt["u0"], np.tile(bt["x0"], (1, 3)))
+    mix = scenes.make_batch(20, seed=2, n_cir=5, n_elp=5, N=5)
+    assert mix["elp"].shape == (20, 5, 5) and mix["u0"].shape == (20, 25)
+
+
+def _shard_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    from alipmpc import sharding
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    B = 10
+    lo, hi = sharding.shard_range(B, rank, world)
+    local = torch.arange(lo, hi, dtype=torch.float64).reshape(-1, 1).repeat(1, 3)
+    full = sharding.gather_to_root(local, B, rank, world)
+    if rank == 0:
+        q.put(full.numpy().tolist())
+    dist.destroy_process_group()
+
+
+def test_sharding_and_gather_gloo_world2():
+    import multiprocessing as mp
+    import socket
+    from alipmpc import sharding
+    assert [sharding.shard_range(10, r, 3) for r in range(3)] == [(0, 4), (4, 7), (7, 10)]
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_shard_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    full = np.array(q.get(timeout=120))
+    for p in ps:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert np.array_equal(full[:, 0], np.arange(10))

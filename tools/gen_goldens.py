@@ -329,6 +329,11 @@ def gen_g2(modi, sig, rand_obs, n_cases):
                 c0 = cs[t % len(cs)]
                 d = np.array([10.0, 10.0]) - c0[:2]
                 d /= np.linalg.norm(d) + 1e-12
+                # off the circle-goal line by 1..10 degrees: exactly collinear starts make the sign of the
+                # reference's (theta - alpha) a matter of atan2 rounding
+                ang = rng.uniform(np.deg2rad(1.0), np.deg2rad(10.0)) * rng.choice([-1, 1])
+                ca, sa = np.cos(ang), np.sin(ang)
+                d = np.array([ca * d[0] - sa * d[1], sa * d[0] + ca * d[1]])
                 pos = c0[:2] - d * (c0[2] + 0.3 + 0.8 * rng.random())
                 x0[:2] = pos
             g = [[10.0, 10.0]] if t % 5 else [[rng.uniform(4, 10), rng.uniform(4, 10)]]
