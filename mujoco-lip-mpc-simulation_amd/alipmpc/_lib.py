@@ -49,11 +49,14 @@ def load(build_if_missing=True):
     global _lib
     if _lib is not None:
         return _lib
-    if build_if_missing and _build.needs_build():
-        _build.build()
-    if not os.path.exists(_build.LIB):
-        raise RuntimeError(f"libalipmpc.so not found at {_build.LIB}; run alipmpc.build.build()")
-    L = ctypes.CDLL(_build.LIB)
+    path = os.environ.get("ALIPMPC_LIB")          # dev override (e.g. the phase-stamp diagnostic build)
+    if path is None:
+        if build_if_missing and _build.needs_build():
+            _build.build()
+        path = _build.LIB
+    if not os.path.exists(path):
+        raise RuntimeError(f"libalipmpc.so not found at {path}; run alipmpc.build.build()")
+    L = ctypes.CDLL(path)
     P = ctypes.c_void_p
     L.alipmpc_default_cfg.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(Cfg)]
     L.alipmpc_default_cfg.restype = ctypes.c_int

@@ -84,6 +84,30 @@ constexpr int KP_DOUBLES = (int)((sizeof(KP) + 15) / 16 * 2);
 
 enum RowType { R_VBX = 0, R_VBY, R_CIR, R_ELP, R_LEG, R_DTH, R_FEN, R_NONE };
 
+// ---- diagnostic phase timers (compiled only with -DALIP_STAMPS; never in the product build)
+#ifdef ALIP_STAMPS
+constexpr int NSTAMP = 10;
+__device__ unsigned long long g_stamps[NSTAMP];
+#define STAMP_DECL unsigned long long st_acc[NSTAMP] = {}; unsigned long long st_t = __builtin_amdgcn_s_memtime();
+#define STAMP(i)                                                              \
+    do {                                                                      \
+        __builtin_amdgcn_sched_barrier(0);                                    \
+        unsigned long long t_ = __builtin_amdgcn_s_memtime();                 \
+        st_acc[i] += t_ - st_t;                                               \
+        st_t = t_;                                                            \
+        __builtin_amdgcn_sched_barrier(0);                                    \
+    } while (0)
+#define STAMP_FLUSH                                                           \
+    do {                                                                      \
+        if (lane_id() == 0)                                                   \
+            for (int i_ = 0; i_ < NSTAMP; ++i_) atomicAdd(&g_stamps[i_], st_acc[i_]); \
+    } while (0)
+#else
+#define STAMP_DECL
+#define STAMP(i) do {} while (0)
+#define STAMP_FLUSH do {} while (0)
+#endif
+
 template <int N>
 struct Dim {
     static constexpr int n = 3 * N;     // decision = footholds p_0..p_{N-1} (see build_tables)
@@ -103,11 +127,11 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & (WAVE - 1); }
 
 __device__ __forceinline__ void wave_sync()
 {
-    // LDS hand-off between lanes of ONE wave: drain this wave's LDS ops and stop the compiler from
-    // moving accesses across.  (No s_barrier: the 4 waves of a block run different instances.)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    // LDS hand-off between lanes of ONE wave.  A wavefront's DS instructions execute in order, so no
+    // s_waitcnt / s_barrier is needed — only a compiler barrier that keeps the accesses in program order.
+    // (The 4 waves of a workgroup run different instances and never synchronise with each other.)
     __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    asm volatile("" ::: "memory");
 }
 
 __device__ __forceinline__ double bcast(double v, int src)
@@ -117,40 +141,72 @@ __device__ __forceinline__ double bcast(double v, int src)
     return __hiloint2double(hi, lo);
 }
 
-__device__ __forceinline__ double wsum(double v)
+// ---- cross-lane exchange without LDS: DPP within 16-lane rows, permlane swaps across rows
+template <int CTRL>
+__device__ __forceinline__ double dpp(double v)
 {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-    return v;
+    int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+    int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
 }
+// returns (v[l], v[l ^ 16]) / (v[l], v[l ^ 32]) as the symmetric pair (a, b)
+__device__ __forceinline__ void swap16(double v, double& a, double& b)
+{
+    auto lo = __builtin_amdgcn_permlane16_swap((unsigned)__double2loint(v), (unsigned)__double2loint(v), false, false);
+    auto hi = __builtin_amdgcn_permlane16_swap((unsigned)__double2hiint(v), (unsigned)__double2hiint(v), false, false);
+    a = __hiloint2double((int)hi[0], (int)lo[0]);
+    b = __hiloint2double((int)hi[1], (int)lo[1]);
+}
+__device__ __forceinline__ void swap32(double v, double& a, double& b)
+{
+    auto lo = __builtin_amdgcn_permlane32_swap((unsigned)__double2loint(v), (unsigned)__double2loint(v), false, false);
+    auto hi = __builtin_amdgcn_permlane32_swap((unsigned)__double2hiint(v), (unsigned)__double2hiint(v), false, false);
+    a = __hiloint2double((int)hi[0], (int)lo[0]);
+    b = __hiloint2double((int)hi[1], (int)lo[1]);
+}
+
+struct OpAdd {
+    __device__ double operator()(double a, double b) const { return a + b; }
+};
+struct OpMax {
+    __device__ double operator()(double a, double b) const { return fmax(a, b); }
+};
+struct OpMin {
+    __device__ double operator()(double a, double b) const { return fmin(a, b); }
+};
+
+// butterfly over all 64 lanes; every lane receives the result.
+//   quad_perm [1,0,3,2] (l^1), quad_perm [2,3,0,1] (l^2), row_half_mirror (quads of a half-row),
+//   row_mirror (half-rows), permlane16_swap (l^16), permlane32_swap (l^32)
+template <class Op>
+__device__ __forceinline__ double wreduce(double v, Op op)
+{
+    v = op(v, dpp<0xB1>(v));
+    v = op(v, dpp<0x4E>(v));
+    v = op(v, dpp<0x141>(v));
+    v = op(v, dpp<0x140>(v));
+    double a, b;
+    swap16(v, a, b);
+    v = op(a, b);
+    swap32(v, a, b);
+    return op(a, b);
+}
+__device__ __forceinline__ double wsum(double v) { return wreduce(v, OpAdd()); }
+__device__ __forceinline__ double wmax(double v) { return wreduce(v, OpMax()); }
+__device__ __forceinline__ double wmin(double v) { return wreduce(v, OpMin()); }
 __device__ __forceinline__ void wsum2(double& a, double& b)
 {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        double ta = __shfl_xor(a, o);
-        double tb = __shfl_xor(b, o);
-        a += ta;
-        b += tb;
-    }
-}
-__device__ __forceinline__ double wmax(double v)
-{
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = fmax(v, __shfl_xor(v, o));
-    return v;
-}
-__device__ __forceinline__ double wmin(double v)
-{
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = fmin(v, __shfl_xor(v, o));
-    return v;
+    a = wsum(a);
+    b = wsum(b);
 }
 // sum over the 4 lane groups (lanes c, c+16, c+32, c+48)
 __device__ __forceinline__ double gsum(double v)
 {
-    v += __shfl_xor(v, 16);
-    v += __shfl_xor(v, 32);
-    return v;
+    double a, b;
+    swap16(v, a, b);
+    v = a + b;
+    swap32(v, a, b);
+    return a + b;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -757,13 +813,14 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
     wsum2(th0, nbl);
     const double m_act = wsum(mal);
     const double theta_max = 1e4 * fmax(1.0, th0), theta_min = 1e-4 * fmax(1.0, th0);
-    double fth[2] = {INFINITY, INFINITY}, fph[2] = {INFINITY, INFINITY};
+    double fth0 = INFINITY, fph0 = INFINITY, fth1 = INFINITY, fph1 = INFINITY;   // filter entries lane, lane+64
     int nf = 0;
     double dw_last = 0.0;
     int status = -1, it = 0, n_rest = 0;
     double e0 = INFINITY;
     const double gth = 1e-5, gph = 1e-8, sth = 1.1, sph = 2.3, eta = 1e-8, gal = 0.05;
 
+    STAMP_DECL
     for (it = 0; it <= P.max_iter; ++it) {
         double f = 0.0, gfc[NT], ryc[NT];
         bool reeval = false;
@@ -790,6 +847,7 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
                 }
                 wave_sync();
             }
+            STAMP(0);
             // ---- grad f and J^T y in the MFMA lane layout (column = lane & 15), reduced over the 4 groups
 #pragma unroll
             for (int T = 0; T < NT; ++T) {
@@ -812,6 +870,7 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
                 gfc[T] = gsum(gfc[T]);
                 ryc[T] = gsum(ryc[T]);
             }
+            STAMP(1);
             if (reeval) break;
             // ---- convergence test (IPOPT scaled overall error) and barrier update
             double ru = 0.0;
@@ -866,6 +925,7 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
             }
             break;
         }
+        STAMP(2);
         if (status == 0 || it == P.max_iter) break;
         const double tau = fmax(0.99, 1.0 - mu);
 
@@ -882,6 +942,7 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
                 w.rw[r] = (hl[q] ? mu / dl : 0.0) - (hu[q] ? mu / du : 0.0) - sg * rcv[q];
             }
         }
+        STAMP(3);
         hess_pass<N>(P, w, eps, gxg, gyg);
         wave_sync();
         double rhsc[NT];
@@ -942,6 +1003,7 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
             }
         }
         wave_sync();
+        STAMP(4);
         // ---- factor with inertia correction, solve for du
         double xv;
         {
@@ -988,6 +1050,7 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
                 acc += lane < i ? w.K[i * KLD + (lane & 31)] * xi : 0.0;
             }
         }
+        STAMP(5);
         // ---- dV = G du  (du staged through LDS, read as broadcasts)
         if (lane < n) w.Vt[lane] = xv;
         wave_sync();
@@ -1044,6 +1107,7 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
             amin = gth;
         }
         amin *= gal;
+        STAMP(6);
         // ---- filter line search on trial points V + a dV
         double a = ap;
         bool accepted = false, ftype = false;
@@ -1078,8 +1142,8 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
             const double pht = anybad ? INFINITY : ft - mu * lg;
             bool ok = isfinite(pht) && tht < theta_max;
             if (ok) {
-                const bool b0 = lane < nf && !(tht < fth[0] || pht < fph[0]);
-                const bool b1 = lane + WAVE < nf && !(tht < fth[1] || pht < fph[1]);
+                const bool b0 = lane < nf && !(tht < fth0 || pht < fph0);
+                const bool b1 = lane + WAVE < nf && !(tht < fth1 || pht < fph1);
                 ok = __ballot(b0 || b1) == 0ull;
             }
             if (ok) {
@@ -1097,12 +1161,18 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
             if (accepted) break;
             a *= 0.5;
         }
+        STAMP(7);
         if (accepted) {
             if (!ftype && nf < FILTER_CAP) {
                 const double vt = (1 - gth) * theta, vp = phi - gph * theta;
                 if ((nf & (WAVE - 1)) == lane) {
-                    fth[nf >> 6] = vt;
-                    fph[nf >> 6] = vp;
+                    if (nf < WAVE) {
+                        fth0 = vt;
+                        fph0 = vp;
+                    } else {
+                        fth1 = vt;
+                        fph1 = vp;
+                    }
                 }
                 nf++;
             }
@@ -1167,7 +1237,10 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
             }
         }
         wave_sync();
+        STAMP(9);
     }
+    STAMP(8);
+    STAMP_FLUSH;
     // ---- status + outputs (violation measured on the reference's exact |.|)
     wave_sync();
     if (status != 0 && status != 2) {
@@ -1762,6 +1835,19 @@ int alipmpc_eval_batch(void* handle, int64_t B, const double* x0, const double* 
     return run_batch((Handle*)handle, false, B, x0, goal, leg, cir, nc, elp, ne, u, nullptr, nullptr, nullptr,
                      nullptr, nullptr, f, grad, c, J, cl, cu, goal_eff, row_active, hip_stream);
 }
+
+#ifdef ALIP_STAMPS
+int alipmpc_dbg_stamps(unsigned long long* out, int reset)
+{
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(alip::g_stamps), sizeof(unsigned long long) * alip::NSTAMP) != hipSuccess)
+        return -1;
+    if (reset) {
+        unsigned long long z[alip::NSTAMP] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(alip::g_stamps), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return alip::NSTAMP;
+}
+#endif
 
 double alipmpc_last_kernel_ms(void* handle)
 {
