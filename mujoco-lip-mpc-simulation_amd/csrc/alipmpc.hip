@@ -48,7 +48,7 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 // kernel parameters (by value)
 // ------------------------------------------------------------------------------------------------
 struct KP {
-    int nc_max, ne_max, rps, m_max, mr4, modi, max_iter, select_obs, detour;
+    int nc_max, ne_max, rps, m_max, mr4, mo4, modi, max_iter, select_obs, detour;
     double tol, acc_tol, q, p, r, gm1, s, detect_r2, leg2, bvx_lo, bvx_hi, bvy_lo, bvy_hi, dth, mu_init;
     const double* G;   // NG x NCP
     const double* E;   // NG x 5
@@ -82,7 +82,7 @@ struct KP {
 
 constexpr int KP_DOUBLES = (int)((sizeof(KP) + 15) / 16 * 2);
 
-enum RowType { R_VBX = 0, R_VBY, R_CIR, R_ELP, R_LEG, R_DTH, R_FEN, R_NONE };
+enum RowType { R_VBX = 0, R_VBY, R_CIR, R_ELP, R_LEG, R_DTH, R_FEN, R_NONE, R_OBJ };
 
 // ---- diagnostic phase timers (compiled only with -DALIP_STAMPS; never in the product build)
 #ifdef ALIP_STAMPS
@@ -132,6 +132,20 @@ __device__ __forceinline__ void wave_sync()
     // (The 4 waves of a workgroup run different instances and never synchronise with each other.)
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
+}
+
+// wave-uniform int (SGPR)
+__device__ __forceinline__ int rfl(int x) { return __builtin_amdgcn_readfirstlane(x); }
+// Opaque copy of a per-lane value: addresses derived from it are recomputed after this point instead of
+// being hoisted out of the interior-point loop (dozens of hoisted LDS addresses otherwise spill).
+#define RELAUNDER(x) asm volatile("" : "+v"(x))
+
+// a wave-uniform double: pins it to an SGPR pair (long-lived uniform values otherwise occupy VGPRs)
+__device__ __forceinline__ double uni(double v)
+{
+    const int lo = __builtin_amdgcn_readfirstlane(__double2loint(v));
+    const int hi = __builtin_amdgcn_readfirstlane(__double2hiint(v));
+    return __hiloint2double(hi, lo);
 }
 
 __device__ __forceinline__ double bcast(double v, int src)
@@ -189,7 +203,7 @@ __device__ __forceinline__ double wreduce(double v, Op op)
     swap16(v, a, b);
     v = op(a, b);
     swap32(v, a, b);
-    return op(a, b);
+    return uni(op(a, b));
 }
 __device__ __forceinline__ double wsum(double v) { return wreduce(v, OpAdd()); }
 __device__ __forceinline__ double wmax(double v) { return wreduce(v, OpMax()); }
@@ -475,89 +489,6 @@ __device__ double state_pass(const KP& P, const double* V, double* CT, double* S
     return fk;
 }
 
-// ------------------------------------------------------------------------------------------------
-// Hessian blocks: lane kb (0..N) writes S block kb (8x8, symmetric) of L = f - y^T c
-// ------------------------------------------------------------------------------------------------
-template <int N>
-__device__ void hess_pass(const KP& P, const WS<N>& w, double eps, double gxg, double gyg)
-{
-    const int lane = lane_id();
-    if (lane > N) return;
-    const int kb = lane;
-    double* S = w.S + 64 * kb;
-    const double* V = w.V;
-    const int nc_sel = w.nsel[0], ne_sel = w.nsel[1];
-    double h00 = 0, h01 = 0, h11 = 0, h04 = 0, h14 = 0, h44 = 0, h24 = 0, h34 = 0;
-    double h05 = 0, h55 = 0, h77 = 0;
-    const double* qq = w.obs + 3 * P.nc_max + 5 * P.ne_max;
-    if (kb >= 1) {
-        double px = V[gx(kb, 0)], py = V[gx(kb, 1)], th = V[gx(kb, 4)];
-        double wq = P.q + (kb == 1 ? P.p : 0.0);
-        double dxg = gxg - px, dyg = gyg - py;
-        double rho2 = dxg * dxg + dyg * dyg, r4 = rho2 * rho2;
-        double phi = th - atan2(dyg, dxg);
-        double gp0 = -dyg / rho2, gp1 = dxg / rho2;
-        double s00 = 2 * dxg * dyg / r4, s01 = (dyg * dyg - dxg * dxg) / r4, s11 = -2 * dxg * dyg / r4;
-        h00 = 2 * wq + 2 * P.r * (gp0 * gp0 - phi * s00);
-        h01 = 2 * P.r * (gp0 * gp1 - phi * s01);
-        h11 = 2 * wq + 2 * P.r * (gp1 * gp1 - phi * s11);
-        h04 = 2 * P.r * gp0;
-        h14 = 2 * P.r * gp1;
-        h44 = 2 * P.r;
-        // rows of step kb-1 act on x_kb as the post-step state
-        const int base = (kb - 1) * P.rps;
-        double ct = w.CT[kb], st = w.ST[kb];
-        double vx = V[gx(kb, 2)], vy = V[gx(kb, 3)];
-        double vbx = ct * vx + st * vy, vby = -st * vx + ct * vy;
-        double wbx = w.ry[base + 0] + (P.modi ? w.ry[base + P.rps - 1] : 0.0);
-        double wby = w.ry[base + 1];
-        h24 = wbx * st + wby * ct;
-        h34 = -wbx * ct + wby * st;
-        h44 += wbx * vbx + wby * vby;
-        for (int j = 0; j < nc_sel; ++j) {
-            double y = w.ry[base + 2 + j];
-            h00 -= 2 * y;
-            h11 -= 2 * y;
-        }
-        for (int j = 0; j < ne_sel; ++j) {
-            double y = w.ry[base + 2 + P.nc_max + j];
-            h00 -= y * 2 * qq[j];
-            h01 -= y * qq[P.ne_max + j];
-            h11 -= y * 2 * qq[2 * P.ne_max + j];
-        }
-    }
-    if (kb < N) {
-        const int base = kb * P.rps;
-        if (kb >= 1) {
-            for (int j = 0; j < nc_sel; ++j) {
-                double y = w.ry[base + 2 + j] * P.gm1;
-                h00 -= 2 * y;
-                h11 -= 2 * y;
-            }
-            for (int j = 0; j < ne_sel; ++j) {
-                double y = w.ry[base + 2 + P.nc_max + j] * P.gm1;
-                h00 -= y * 2 * qq[j];
-                h01 -= y * qq[P.ne_max + j];
-                h11 -= y * 2 * qq[2 * P.ne_max + j];
-            }
-        }
-        double yl = w.ry[base + 2 + P.nc_max + P.ne_max];
-        h00 -= 2 * yl;
-        h11 -= 2 * yl;
-        h05 = 2 * yl;
-        h55 = -2 * yl;
-        if (P.modi && eps != 0.0) {
-            double a, d1, d2;
-            sabs(V[gp(kb, 2)], eps, a, d1, d2);
-            h77 = -w.ry[base + P.rps - 1] * P.s * d2;
-        }
-    }
-    S[0 * 8 + 0] = h00; S[0 * 8 + 1] = h01; S[1 * 8 + 0] = h01; S[1 * 8 + 1] = h11;
-    S[0 * 8 + 4] = h04; S[4 * 8 + 0] = h04; S[1 * 8 + 4] = h14; S[4 * 8 + 1] = h14;
-    S[2 * 8 + 4] = h24; S[4 * 8 + 2] = h24; S[3 * 8 + 4] = h34; S[4 * 8 + 3] = h34; S[4 * 8 + 4] = h44;
-    S[0 * 8 + 5] = h05; S[5 * 8 + 0] = h05; S[1 * 8 + 6] = h05; S[6 * 8 + 1] = h05;
-    S[5 * 8 + 5] = h55; S[6 * 8 + 6] = h55; S[7 * 8 + 7] = h77;
-}
 
 // J[r][col] from the generator form
 __device__ __forceinline__ double jrow_col(const double* rcoef, const uint8_t* rgen, const double* G, int ldg, int r,
@@ -572,8 +503,8 @@ __device__ __forceinline__ double jrow_col(const double* rcoef, const uint8_t* r
 // ------------------------------------------------------------------------------------------------
 // instance prologue: load inputs, select_obs, detour goal, ellipse forms, V = E x0 + G u0
 // ------------------------------------------------------------------------------------------------
-template <int N, bool FROM_U>
-__device__ void prologue(const KP& P, const WS<N>& w, const double* G, const double* E, long long b, double& gxg,
+template <int N, bool FROM_U, class WT>
+__device__ void prologue(const KP& P, const WT& w, const double* G, const double* E, long long b, double& gxg,
                          double& gyg, int& legv, double& uj)
 {
     using D = Dim<N>;
@@ -741,9 +672,283 @@ __device__ __forceinline__ bool chol_rows(double (&a)[n], double& myidg, int lan
 }
 
 // ------------------------------------------------------------------------------------------------
-// the solve kernel: one instance per wave
+// solve-kernel workspace.  Rows r < mr4 are the padded constraint rows; rows mr4 .. mr4+N-1 are the
+// objective terms f_k (k = 1..N) treated as pseudo-rows ("OBJ rows"): same generator-form gradient, so
+// grad f and J^T y come out of ONE J-layout sweep, and grad f . dV out of the row-layout dS pass.
+// mo4 = mr4 + 4 ceil(N/4) rows in total.
 // ------------------------------------------------------------------------------------------------
-template <int N, int RPL>
+template <int N>
+struct WSS {
+    double* V;      // NG   current generator values (canonical copy; rows keep register copies)
+    double* Vt;     // NG   prologue scratch
+    double* dV;     // NG   step
+    double* CT;     // N+1  cos / sin of theta_k at V (written by the VBX rows, read by the Hessian lanes)
+    double* ST;     // N+1
+    double* S;      // (N+1) x 64 Hessian blocks
+    double* hobj;   // (N+1) x 6 objective Hessian parts (written by the OBJ rows)
+    double* rcoef;  // mo4 x 4
+    double* cst;    // 16 per-instance constants read at use (keeps long-lived uniforms out of registers)
+    double* ry;     // mo4   y (constraint rows), -1 (OBJ rows)
+    double* rsig;   // mo4   Sigma
+    double* rw;     // mo4   rhs weights (OBJ rows: -1)
+    double* obs;    // prologue layout: circles 3*nc_max, ellipses 5*ne_max, then qa, qb, qc, ek (4*ne_max)
+    double* obs6;   // (nc_max + ne_max) x 6 unified quadratic form [ox, oy, qa, qb, qc, ek] per row slot
+    double* K;      // NCP x KLD
+    double* rclo;   // mr4 original bounds (status / infeasibility checks only)
+    double* rcuo;   // mr4
+    int* nsel;      // [0] = nc_sel, [1] = ne_sel
+    uint32_t* rgen; // mo4 packed generator indices (4 x 8 bit)
+};
+
+template <int N>
+__host__ __device__ constexpr int wss_doubles(int nc_max, int ne_max, int mr4, int mo4)
+{
+    int d = 16 + 3 * Dim<N>::NG + 2 * (N + 1) + 64 * (N + 1) + 6 * (N + 1) + 4 * mo4 + 3 * mo4 + 3 * nc_max +
+            9 * ne_max + 6 * (nc_max + ne_max) + 6 + Dim<N>::NCP * Dim<N>::KLD + 2 * mr4 + 1 + (mo4 + 1) / 2;
+    return (d + 3) & ~3;   // 32-byte multiple: rcoef rows are read as 2 x b128
+}
+
+template <int N>
+__device__ WSS<N> carve_s(double* base, int nc_max, int ne_max, int mr4, int mo4)
+{
+    using D = Dim<N>;
+    WSS<N> w;
+    double* p = base;
+    w.rcoef = p; p += 4 * mo4;   // first: 32-byte aligned
+    w.cst = p; p += 16;
+    w.V = p; p += D::NG;
+    w.Vt = p; p += D::NG;
+    w.dV = p; p += D::NG;
+    w.CT = p; p += N + 1;
+    w.ST = p; p += N + 1;
+    w.S = p; p += 64 * (N + 1);
+    w.hobj = p; p += 6 * (N + 1);
+    w.ry = p; p += mo4;
+    w.rsig = p; p += mo4;
+    w.rw = p; p += mo4;
+    w.obs = p; p += 3 * nc_max + 9 * ne_max;
+    w.obs6 = p; p += 6 * (nc_max + ne_max) + 6;
+    w.K = p; p += D::NCP * D::KLD;
+    w.rclo = p; p += mr4;
+    w.rcuo = p; p += mr4;
+    w.nsel = reinterpret_cast<int*>(p); p += 1;
+    w.rgen = reinterpret_cast<uint32_t*>(p);
+    return w;
+}
+
+// generator rows a row reads: VEL rows [vx, vy, theta of x_{k+1}, turn p_k], obstacle rows
+// [px, py of x_{k+1}, px, py of x_k], LEG [px, py of x_k, foot x, y of p_k], DTH [-, -, -, turn p_k],
+// OBJ [px, py, theta of x_k, -]
+__device__ __forceinline__ uint32_t row_gens(int type, int k)
+{
+    int g0 = 0, g1 = 0, g2 = 0, g3 = 0;
+    switch (type) {
+    case R_VBX:
+    case R_VBY:
+    case R_FEN:
+        g0 = gx(k + 1, 2); g1 = gx(k + 1, 3); g2 = gx(k + 1, 4); g3 = gp(k, 2);
+        break;
+    case R_CIR:
+    case R_ELP:
+        g0 = gx(k + 1, 0); g1 = gx(k + 1, 1); g2 = gx(k, 0); g3 = gx(k, 1);
+        break;
+    case R_LEG:
+        g0 = gx(k, 0); g1 = gx(k, 1); g2 = gp(k, 0); g3 = gp(k, 1);
+        break;
+    case R_DTH:
+        g3 = gp(k, 2);
+        break;
+    case R_OBJ:
+        g0 = gx(k, 0); g1 = gx(k, 1); g2 = gx(k, 4);
+        break;
+    default:
+        break;
+    }
+    return (uint32_t)g0 | ((uint32_t)g1 << 8) | ((uint32_t)g2 << 16) | ((uint32_t)g3 << 24);
+}
+
+__device__ __forceinline__ int gen_i(uint32_t pk, int i) { return (int)((pk >> (8 * i)) & 255u); }
+
+// the transcendental part of a row: VEL rows sincos(theta_{k+1}) -> (a0, a1) = (sin, cos);
+// OBJ rows phi = theta_k - atan2(goal - p) -> a0.  (Computed for every lane; lanes keep what they need.)
+__device__ __forceinline__ void row_trans(int type, const double (&v)[4], double gxg, double gyg, double& a0, double& a1)
+{
+    double s_, c_;
+    sincos(v[2], &s_, &c_);
+    const double at = atan2(gyg - v[1], gxg - v[0]);
+    a0 = type == R_OBJ ? v[2] - at : s_;
+    a1 = c_;
+}
+
+struct RowK {   // uniform constants of the row functions
+    double gm1, s, q, p, r, gxg, gyg;
+};
+// cst slots
+enum { K_GM1 = 0, K_S, K_Q, K_P, K_R, K_GXG, K_GYG, K_THMAX, K_THMIN, K_MACT, K_NBL, K_TOL, K_ACCTOL };
+__device__ __forceinline__ RowK load_rowk(const double* cst)
+{
+    RowK C;
+    C.gm1 = cst[K_GM1]; C.s = cst[K_S]; C.q = cst[K_Q]; C.p = cst[K_P]; C.r = cst[K_R];
+    C.gxg = cst[K_GXG]; C.gyg = cst[K_GYG];
+    return C;
+}
+
+// value of row `type` at generator values v (branch-free: every family is computed, one is selected)
+__device__ __forceinline__ double row_value(int type, int k, const double (&v)[4], double a0, double a1,
+                                            const double (&o)[6], const RowK& C, double eps)
+{
+    // velocity family
+    const bool vby = type == R_VBY;
+    const double ca = vby ? -a0 : a1, cb = vby ? a1 : a0;
+    double fa, fd1, fd2;
+    sabs(v[3], eps, fa, fd1, fd2);
+    const double cvel = ca * v[0] + cb * v[1] + (type == R_FEN ? C.s * fa : 0.0);
+    // D-CBF (circle == ellipse with qa = qc = 1, qb = 0, ek = r^2)
+    const double x1 = v[0] - o[0], y1 = v[1] - o[1], x0 = v[2] - o[0], y0 = v[3] - o[1];
+    const double h1 = o[2] * x1 * x1 + o[3] * x1 * y1 + o[4] * y1 * y1 - o[5];
+    const double h0 = o[2] * x0 * x0 + o[3] * x0 * y0 + o[4] * y0 * y0 - o[5];
+    const double cobs = h1 + C.gm1 * h0;
+    // leg length
+    const double ex = v[0] - v[2], ey = v[1] - v[3];
+    const double cleg = ex * ex + ey * ey;
+    // objective term f_k
+    const double w = C.q + (k == 1 ? C.p : 0.0);
+    const double dxg = C.gxg - v[0], dyg = C.gyg - v[1];
+    const double cobj = w * (dxg * dxg + dyg * dyg) + C.r * a0 * a0;
+    double c = 0.0;
+    c = (type == R_VBX || vby || type == R_FEN) ? cvel : c;
+    c = (type == R_CIR || type == R_ELP) ? cobs : c;
+    c = type == R_LEG ? cleg : c;
+    c = type == R_DTH ? v[3] : c;
+    c = type == R_OBJ ? cobj : c;
+    return c;
+}
+
+// generator-form gradient coefficients of row `type` (OBJ rows: grad f_k; hx = its 6 Hessian parts
+// [h00 h01 h11 h04 h14 h44] on (px, py, theta) of x_k)
+__device__ __forceinline__ void row_coef(int type, int k, const double (&v)[4], double a0, double a1,
+                                         const double (&o)[6], const RowK& C, double eps, double (&cf)[4],
+                                         double (&hx)[6])
+{
+    const bool vby = type == R_VBY, vel = type == R_VBX || vby || type == R_FEN;
+    const bool obs = type == R_CIR || type == R_ELP;
+    // velocity family: d/dtheta of (ca, cb)
+    const double ca = vby ? -a0 : a1, cb = vby ? a1 : a0;
+    const double da = vby ? -a1 : -a0, db = vby ? -a0 : a1;
+    double fa, fd1, fd2;
+    sabs(v[3], eps, fa, fd1, fd2);
+    // D-CBF
+    const double x1 = v[0] - o[0], y1 = v[1] - o[1], x0 = v[2] - o[0], y0 = v[3] - o[1];
+    // leg
+    const double ex = v[0] - v[2], ey = v[1] - v[3];
+    // objective
+    const double w = C.q + (k == 1 ? C.p : 0.0);
+    const double dxg = C.gxg - v[0], dyg = C.gyg - v[1];
+    const double rho2 = dxg * dxg + dyg * dyg, ir2 = 1.0 / rho2;
+    const double gp0 = -dyg * ir2, gp1 = dxg * ir2, phi = a0;
+    double c0 = 0.0, c1 = 0.0, c2 = 0.0, c3 = 0.0;
+    if (vel) {
+        c0 = ca; c1 = cb; c2 = da * v[0] + db * v[1]; c3 = type == R_FEN ? C.s * fd1 : 0.0;
+    }
+    if (obs) {
+        c0 = 2 * o[2] * x1 + o[3] * y1; c1 = 2 * o[4] * y1 + o[3] * x1;
+        c2 = C.gm1 * (2 * o[2] * x0 + o[3] * y0); c3 = C.gm1 * (2 * o[4] * y0 + o[3] * x0);
+    }
+    if (type == R_LEG) {
+        c0 = 2 * ex; c1 = 2 * ey; c2 = -2 * ex; c3 = -2 * ey;
+    }
+    if (type == R_DTH) c3 = 1.0;
+    if (type == R_OBJ) {
+        c0 = -2 * w * dxg + 2 * C.r * phi * gp0;
+        c1 = -2 * w * dyg + 2 * C.r * phi * gp1;
+        c2 = 2 * C.r * phi;
+        const double ir4 = ir2 * ir2;
+        const double s00 = 2 * dxg * dyg * ir4, s01 = (dyg * dyg - dxg * dxg) * ir4, s11 = -2 * dxg * dyg * ir4;
+        hx[0] = 2 * w + 2 * C.r * (gp0 * gp0 - phi * s00);
+        hx[1] = 2 * C.r * (gp0 * gp1 - phi * s01);
+        hx[2] = 2 * w + 2 * C.r * (gp1 * gp1 - phi * s11);
+        hx[3] = 2 * C.r * gp0;
+        hx[4] = 2 * C.r * gp1;
+        hx[5] = 2 * C.r;
+    }
+    cf[0] = c0; cf[1] = c1; cf[2] = c2; cf[3] = c3;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Hessian blocks of L = f - y^T c: lane kb (0..N) writes S block kb (8x8, symmetric).  Objective parts
+// come from the OBJ rows (hobj), everything else from y and the obstacle forms.
+// ------------------------------------------------------------------------------------------------
+template <int N>
+__device__ void hess_blocks(const WSS<N>& w, double eps, int lane, int rps, int nobs, int modi)
+{
+    if (lane > N) return;
+    const double gm1 = w.cst[K_GM1], s_fen = w.cst[K_S];
+    const int kb = lane;
+    double h00 = 0, h01 = 0, h11 = 0, h04 = 0, h14 = 0, h44 = 0, h24 = 0, h34 = 0;
+    double h05 = 0, h55 = 0, h77 = 0;
+    if (kb >= 1) {
+        const double* ho = w.hobj + 6 * kb;
+        h00 = ho[0]; h01 = ho[1]; h11 = ho[2]; h04 = ho[3]; h14 = ho[4]; h44 = ho[5];
+        // rows of step kb-1 act on x_kb as the post-step state
+        const int base = (kb - 1) * rps;
+        const double ct = w.CT[kb], st = w.ST[kb];
+        const double vx = w.V[gx(kb, 2)], vy = w.V[gx(kb, 3)];
+        const double vbx = ct * vx + st * vy, vby = -st * vx + ct * vy;
+        const double wbx = w.ry[base + 0] + (modi ? w.ry[base + rps - 1] : 0.0);
+        const double wby = w.ry[base + 1];
+        h24 = wbx * st + wby * ct;
+        h34 = -wbx * ct + wby * st;
+        h44 += wbx * vbx + wby * vby;
+        // inactive slots have y = 0 and a zero form
+#pragma unroll 4
+        for (int j = 0; j < nobs; ++j) {
+            const double y = w.ry[base + 2 + j];
+            const double* o = w.obs6 + 6 * j;
+            h00 -= 2 * y * o[2];
+            h01 -= y * o[3];
+            h11 -= 2 * y * o[4];
+        }
+    }
+    if (kb < N) {
+        const int base = kb * rps;
+        if (kb >= 1) {
+#pragma unroll 4
+            for (int j = 0; j < nobs; ++j) {
+                const double y = w.ry[base + 2 + j] * gm1;
+                const double* o = w.obs6 + 6 * j;
+                h00 -= 2 * y * o[2];
+                h01 -= y * o[3];
+                h11 -= 2 * y * o[4];
+            }
+        }
+        const double yl = w.ry[base + 2 + nobs];
+        h00 -= 2 * yl;
+        h11 -= 2 * yl;
+        h05 = 2 * yl;
+        h55 = -2 * yl;
+        if (modi && eps != 0.0) {
+            double a, d1, d2;
+            sabs(w.V[gp(kb, 2)], eps, a, d1, d2);
+            h77 = -w.ry[base + rps - 1] * s_fen * d2;
+        }
+    }
+    double* S = w.S + 64 * kb;
+    S[0 * 8 + 0] = h00; S[0 * 8 + 1] = h01; S[1 * 8 + 0] = h01; S[1 * 8 + 1] = h11;
+    S[0 * 8 + 4] = h04; S[4 * 8 + 0] = h04; S[1 * 8 + 4] = h14; S[4 * 8 + 1] = h14;
+    S[2 * 8 + 4] = h24; S[4 * 8 + 2] = h24; S[3 * 8 + 4] = h34; S[4 * 8 + 3] = h34; S[4 * 8 + 4] = h44;
+    S[0 * 8 + 5] = h05; S[5 * 8 + 0] = h05; S[1 * 8 + 6] = h05; S[6 * 8 + 1] = h05;
+    S[5 * 8 + 5] = h55; S[6 * 8 + 6] = h55; S[7 * 8 + 7] = h77;
+}
+
+// ------------------------------------------------------------------------------------------------
+// the solve kernel: one instance per wave.
+//   Row layout (lane r = row r [+ 64]): values, multipliers, slacks, bound terms, and a REGISTER copy of
+//   the 4 generator values each row reads (rv) and of their step (rdv), so line-search trial points
+//   V + a dV are evaluated without touching LDS.  The canonical V lives in LDS (lane t owns V[t]).
+//   J layout (lane = (g4, col), rows 4s + g4, KSM steps, fully unrolled): J^T y, grad f, J^T w and the
+//   MFMA KKT products.
+// ------------------------------------------------------------------------------------------------
+template <int N, int KSM>
 __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
 {
     using D = Dim<N>;
@@ -752,67 +957,157 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
     constexpr int NCP = D::NCP;
     constexpr int NG = D::NG;
     constexpr int KLD = D::KLD;
+    constexpr int RPL = (4 * KSM + WAVE - 1) / WAVE;
+    constexpr bool JC = KSM * NT <= 16;   // keep the J tile in registers between the two J-layout passes
+    static_assert(NG <= WAVE, "one generator row per lane");
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    // kernel parameters live in LDS: keeps ~90 kernarg SGPRs from being pinned across the solve
     KP* Ps = reinterpret_cast<KP*>(smem);
     double* G = smem + KP_DOUBLES;
     double* E = G + NG * NCP;
-    double* wsb = E + NG * 5 + ((NG * 5) & 1);
+    double* wsb = E + ((NG * 5 + 3) & ~3);
     if (threadIdx.x == 0) *Ps = Pv;
     for (int i = threadIdx.x; i < NG * NCP; i += blockDim.x) G[i] = Pv.G[i];
     for (int i = threadIdx.x; i < NG * 5; i += blockDim.x) E[i] = Pv.E[i];
     __syncthreads();
     const KP& P = *Ps;
-    const int wv = threadIdx.x / WAVE;
-    const int lane = lane_id();
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);   // wave-uniform (SGPR)
+    int lane = lane_id();
     const long long b = (long long)blockIdx.x * WAVES_PER_BLOCK + wv;
     if (b >= P.B) return;
-    WS<N> w = carve<N>(wsb + (size_t)wv * ws_doubles<N>(P.nc_max, P.ne_max, P.mr4), P.nc_max, P.ne_max, P.mr4);
+    // uniform problem sizes in SGPRs (P lives in LDS: a plain read would be a per-lane VGPR value)
+    const int mr4 = rfl(P.mr4), mo4 = rfl(P.mo4), m_max = rfl(P.m_max), rps = rfl(P.rps);
+    const int nc_max = rfl(P.nc_max), ne_max = rfl(P.ne_max), nobs = nc_max + ne_max;
+    const int modi = rfl(P.modi), max_iter = rfl(P.max_iter);
+    WSS<N> w = carve_s<N>(wsb + (size_t)wv * wss_doubles<N>(nc_max, ne_max, mr4, mo4), nc_max, ne_max, mr4, mo4);
     for (int i = lane; i < 64 * (N + 1); i += WAVE) w.S[i] = 0.0;
 
     double gxg, gyg, uj;
     int legv;
     prologue<N, false>(P, w, G, E, b, gxg, gyg, legv, uj);
     const int nc_sel = w.nsel[0], ne_sel = w.nsel[1];
-    const int g4 = lane >> 4, col = lane & 15;
-
-    RowInfo ri[RPL];
-    double cl[RPL], cu[RPL], clo[RPL], cuo[RPL], cr[RPL], sr[RPL], zl[RPL], zu[RPL];
-    bool hl[RPL], hu[RPL];
-    double mu = P.mu_init;
-    double eps = P.modi ? 0.1 * sqrt(mu) : 0.0;
-    state_pass<N, false>(P, w.V, w.CT, w.ST, w.gfg, gxg, gyg);
+    // unified quadratic forms per obstacle row slot (zero form for unused slots)
+    {
+        for (int j = lane; j <= nobs; j += WAVE) {
+            double o[6] = {0, 0, 0, 0, 0, 0};
+            if (j < nc_max) {
+                if (j < nc_sel) {
+                    const double* c = w.obs + 3 * j;
+                    o[0] = c[0]; o[1] = c[1]; o[2] = 1.0; o[4] = 1.0; o[5] = c[2] * c[2];
+                }
+            } else if (j < nobs) {
+                const int e = j - nc_max;
+                if (e < ne_sel) {
+                    const double* el = w.obs + 3 * nc_max + 5 * e;
+                    const double* qq = w.obs + 3 * nc_max + 5 * ne_max;
+                    o[0] = el[0]; o[1] = el[1];
+                    o[2] = qq[e]; o[3] = qq[ne_max + e]; o[4] = qq[2 * ne_max + e]; o[5] = qq[3 * ne_max + e];
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 6; ++i) w.obs6[6 * j + i] = o[i];
+        }
+    }
+    int g4 = lane >> 4, col = lane & 15;
+    // per-row bound flags are recomputed at use (hoisted lane masks would pin ~2 SGPRs each)
+#define HL(q) (cl[q] != -INFINITY)
+#define HU(q) (cu[q] != INFINITY)
+#define RELANE()                        \
+    do {                                \
+        RELAUNDER(lane);                \
+        g4 = lane >> 4;                 \
+        col = lane & 15;                \
+        for (int q_ = 0; q_ < RPL; ++q_) { \
+            RELAUNDER(rtype[q_]);       \
+            RELAUNDER(rk[q_]);          \
+            RELAUNDER(roi[q_]);         \
+            RELAUNDER(rg[q_]);          \
+            RELAUNDER(cl[q_]);          \
+            RELAUNDER(cu[q_]);          \
+        }                               \
+    } while (0)
+    if (lane == 0) {
+        w.cst[K_GM1] = P.gm1; w.cst[K_S] = P.s; w.cst[K_Q] = P.q; w.cst[K_P] = P.p; w.cst[K_R] = P.r;
+        w.cst[K_GXG] = gxg; w.cst[K_GYG] = gyg; w.cst[K_TOL] = P.tol; w.cst[K_ACCTOL] = P.acc_tol;
+    }
     wave_sync();
-    double th0 = 0.0, nbl = 0.0, mal = 0.0;
+#define CK load_rowk(w.cst)
+
+    // ---- per-row state (registers)
+    int rtype[RPL], rk[RPL], roi[RPL];
+    uint32_t rg[RPL];
+    double cl[RPL], cu[RPL], rv[RPL][4], rdv[RPL][4], ra0[RPL], ra1[RPL];
+    double cr[RPL], sr[RPL], zl[RPL], zu[RPL], idl[RPL], idu[RPL];
+    double mu = uni(P.mu_init);
+    double eps = modi ? 0.1 * sqrt(mu) : 0.0;
+    double vme = lane < NG ? w.V[lane] : 0.0, dvme = 0.0;   // lane t's generator value / step
+    double th0 = 0.0, nbl = 0.0, mal = 0.0, fo = 0.0, lg0 = 0.0;
+    wave_sync();
 #pragma unroll
     for (int q = 0; q < RPL; ++q) {
         const int r = lane + WAVE * q;
-        ri[q] = decode_row(P, r, nc_sel, ne_sel);
-        row_bounds(P, ri[q], legv, clo[q], cuo[q]);
-        hl[q] = isfinite(clo[q]);
-        hu[q] = isfinite(cuo[q]);
-        nbl += (double)hl[q] + (double)hu[q];
-        mal += ri[q].type != R_NONE ? 1.0 : 0.0;
-        cl[q] = hl[q] ? clo[q] - 1e-8 * fmax(1.0, fabs(clo[q])) : -INFINITY;
-        cu[q] = hu[q] ? cuo[q] + 1e-8 * fmax(1.0, fabs(cuo[q])) : INFINITY;
-        cr[q] = row_eval<N, false>(P, ri[q], w.V, w.CT, w.ST, w.obs, eps, nullptr, nullptr);
+        RowInfo ri;
+        ri.type = R_NONE; ri.k = 0; ri.slot = 0;
+        if (r < m_max) {
+            ri = decode_row(P, r, nc_sel, ne_sel);
+        } else if (r >= mr4 && r < mr4 + N) {
+            ri.type = R_OBJ;
+            ri.k = r - mr4 + 1;
+        }
+        rtype[q] = ri.type;
+        rk[q] = ri.k;
+        roi[q] = ri.type == R_CIR ? ri.slot : (ri.type == R_ELP ? nc_max + ri.slot : 0);
+        rg[q] = row_gens(ri.type, ri.k);
+        if (r < mo4) w.rgen[r] = rg[q];
+        double clo, cuo;
+        row_bounds(P, ri, legv, clo, cuo);
+        if (r < mr4) {
+            w.rclo[r] = clo;
+            w.rcuo[r] = cuo;
+        }
+        nbl += (double)isfinite(clo) + (double)isfinite(cuo);
+        mal += ri.type < R_NONE ? 1.0 : 0.0;
+        cl[q] = isfinite(clo) ? clo - 1e-8 * fmax(1.0, fabs(clo)) : -INFINITY;
+        cu[q] = isfinite(cuo) ? cuo + 1e-8 * fmax(1.0, fabs(cuo)) : INFINITY;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            rv[q][i] = w.V[gen_i(rg[q], i)];
+            rdv[q][i] = 0.0;
+        }
+        double o[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) o[i] = w.obs6[6 * roi[q] + i];
+        row_trans(rtype[q], rv[q], w.cst[K_GXG], w.cst[K_GYG], ra0[q], ra1[q]);
+        cr[q] = row_value(rtype[q], rk[q], rv[q], ra0[q], ra1[q], o, CK, eps);
         double v = cr[q];
-        const double pl = hl[q] ? fmin(1e-2 * fmax(1.0, fabs(cl[q])), 1e-2 * (cu[q] - cl[q])) : 0.0;
-        const double pu = hu[q] ? fmin(1e-2 * fmax(1.0, fabs(cu[q])), 1e-2 * (cu[q] - cl[q])) : 0.0;
-        if (hl[q] && hu[q])
+        const double pl = HL(q) ? fmin(1e-2 * fmax(1.0, fabs(cl[q])), 1e-2 * (cu[q] - cl[q])) : 0.0;
+        const double pu = HU(q) ? fmin(1e-2 * fmax(1.0, fabs(cu[q])), 1e-2 * (cu[q] - cl[q])) : 0.0;
+        if (HL(q) && HU(q))
             v = fmin(fmax(v, cl[q] + pl), cu[q] - pu);
-        else if (hl[q])
+        else if (HL(q))
             v = fmax(v, cl[q] + pl);
-        else if (hu[q])
+        else if (HU(q))
             v = fmin(v, cu[q] - pu);
-        sr[q] = v;
-        zl[q] = hl[q] ? 1.0 : 0.0;
-        zu[q] = hu[q] ? 1.0 : 0.0;
-        th0 += fabs(cr[q] - sr[q]);
+        sr[q] = rtype[q] < R_NONE ? v : 0.0;
+        zl[q] = HL(q) ? 1.0 : 0.0;
+        zu[q] = HU(q) ? 1.0 : 0.0;
+        const double dl = sr[q] - cl[q], du = cu[q] - sr[q];
+        idl[q] = HL(q) ? 1.0 / dl : 0.0;
+        idu[q] = HU(q) ? 1.0 / du : 0.0;
+        lg0 += HL(q) ? (HU(q) ? log(dl * du) : log(dl)) : (HU(q) ? log(du) : 0.0);
+        if (rtype[q] < R_NONE) th0 += fabs(cr[q] - sr[q]);
+        if (rtype[q] == R_OBJ) fo += cr[q];
     }
     wsum2(th0, nbl);
-    const double m_act = wsum(mal);
-    const double theta_max = 1e4 * fmax(1.0, th0), theta_min = 1e-4 * fmax(1.0, th0);
+    wsum2(fo, lg0);
+    mal = wsum(mal);
+    double f_cur = fo, lsum_cur = lg0;
+    if (lane == 0) {
+        w.cst[K_THMAX] = 1e4 * fmax(1.0, th0);
+        w.cst[K_THMIN] = 1e-4 * fmax(1.0, th0);
+        w.cst[K_MACT] = mal;
+        w.cst[K_NBL] = nbl;
+    }
+    wave_sync();
     double fth0 = INFINITY, fph0 = INFINITY, fth1 = INFINITY, fph1 = INFINITY;   // filter entries lane, lane+64
     int nf = 0;
     double dw_last = 0.0;
@@ -821,104 +1116,122 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
     const double gth = 1e-5, gph = 1e-8, sth = 1.1, sph = 2.3, eta = 1e-8, gal = 0.05;
 
     STAMP_DECL
-    for (it = 0; it <= P.max_iter; ++it) {
-        double f = 0.0, gfc[NT], ryc[NT];
+    for (it = 0; it <= max_iter; ++it) {
+        double gl[NT];                                  // J^T y - grad f  (per column, all lanes)
+        double jv[JC ? KSM : 1][NT];
         bool reeval = false;
         for (;;) {
-            // ---- evaluation at V
-            {
-                const double fk = state_pass<N, true>(P, w.V, w.CT, w.ST, w.gfg, gxg, gyg);
-                f = wsum(fk);
-                wave_sync();
+            RELANE();
+            // ---- row layout: generator-form coefficients at V (OBJ rows: grad f_k and its Hessian parts)
 #pragma unroll
-                for (int q = 0; q < RPL; ++q) {
-                    const int r = lane + WAVE * q;
-                    if (r < P.mr4) {
-                        double cf[4];
-                        int gn[4];
-                        cr[q] = row_eval<N, true>(P, ri[q], w.V, w.CT, w.ST, w.obs, eps, cf, gn);
+            for (int q = 0; q < RPL; ++q) {
+                const int r = lane + WAVE * q;
+                double o[6], cf[4], hx[6];
 #pragma unroll
-                        for (int i = 0; i < 4; ++i) {
-                            w.rcoef[4 * r + i] = cf[i];
-                            w.rgen[4 * r + i] = (uint8_t)gn[i];
-                        }
-                        w.ry[r] = zl[q] - zu[q];
-                    }
+                for (int i = 0; i < 6; ++i) o[i] = w.obs6[6 * roi[q] + i];
+                row_coef(rtype[q], rk[q], rv[q], ra0[q], ra1[q], o, CK, eps, cf, hx);
+                if (r < mo4) {
+                    double2* rc2 = reinterpret_cast<double2*>(w.rcoef + 4 * r);
+                    rc2[0] = make_double2(cf[0], cf[1]);
+                    rc2[1] = make_double2(cf[2], cf[3]);
+                    w.ry[r] = rtype[q] == R_OBJ ? -1.0 : zl[q] - zu[q];
                 }
-                wave_sync();
+                if (rtype[q] == R_VBX) {
+                    w.CT[rk[q] + 1] = ra1[q];
+                    w.ST[rk[q] + 1] = ra0[q];
+                }
+                if (rtype[q] == R_OBJ) {
+#pragma unroll
+                    for (int i = 0; i < 6; ++i) w.hobj[6 * rk[q] + i] = hx[i];
+                }
             }
+            wave_sync();
             STAMP(0);
-            // ---- grad f and J^T y in the MFMA lane layout (column = lane & 15), reduced over the 4 groups
+            RELANE();
+            // ---- J layout: gl = J^T y - grad f (OBJ rows carry y = -1)
 #pragma unroll
-            for (int T = 0; T < NT; ++T) {
-                gfc[T] = 0.0;
-                ryc[T] = 0.0;
-            }
-            for (int s4 = 0; s4 < P.mr4; s4 += 4) {
-                const int r = s4 + g4;
-                const double y = w.ry[r];
+            for (int T = 0; T < NT; ++T) gl[T] = 0.0;
 #pragma unroll
-                for (int T = 0; T < NT; ++T) ryc[T] += jrow_col(w.rcoef, w.rgen, G, NCP, r, 16 * T + col) * y;
-            }
-            for (int t = 4 + g4; t < NG; t += 4) {
-                const double gv = w.gfg[t];
+            for (int s = 0; s < KSM; ++s) {
+                if (4 * s < mo4) {
+                    const int r = 4 * s + g4;
+                    const uint32_t pk = w.rgen[r];
+                    const double2* rc2 = reinterpret_cast<const double2*>(w.rcoef + 4 * r);
+                    const double2 ca = rc2[0], cb = rc2[1];
+                    const double y = w.ry[r];
 #pragma unroll
-                for (int T = 0; T < NT; ++T) gfc[T] += G[t * NCP + 16 * T + col] * gv;
+                    for (int T = 0; T < NT; ++T) {
+                        const int cc = 16 * T + col;
+                        const double j = ca.x * G[gen_i(pk, 0) * NCP + cc] + ca.y * G[gen_i(pk, 1) * NCP + cc] +
+                                         cb.x * G[gen_i(pk, 2) * NCP + cc] + cb.y * G[gen_i(pk, 3) * NCP + cc];
+                        gl[T] += j * y;
+                        if constexpr (JC) jv[JC ? s : 0][T] = j;
+                    }
+                } else if constexpr (JC) {
+#pragma unroll
+                    for (int T = 0; T < NT; ++T) jv[JC ? s : 0][T] = 0.0;
+                }
             }
 #pragma unroll
-            for (int T = 0; T < NT; ++T) {
-                gfc[T] = gsum(gfc[T]);
-                ryc[T] = gsum(ryc[T]);
-            }
+            for (int T = 0; T < NT; ++T) gl[T] = gsum(gl[T]);
             STAMP(1);
             if (reeval) break;
             // ---- convergence test (IPOPT scaled overall error) and barrier update
+            RELANE();
             double ru = 0.0;
 #pragma unroll
             for (int T = 0; T < NT; ++T)
-                if (g4 == 0 && 16 * T + col < n) ru = fmax(ru, fabs(gfc[T] - ryc[T]));
+                if (g4 == 0 && 16 * T + col < n) ru = fmax(ru, fabs(gl[T]));
             double rcm = 0.0, nz = 0.0, comp0 = 0.0;
 #pragma unroll
             for (int q = 0; q < RPL; ++q) {
-                const double dl = hl[q] ? sr[q] - cl[q] : 1.0, du = hu[q] ? cu[q] - sr[q] : 1.0;
-                if (ri[q].type != R_NONE) rcm = fmax(rcm, fabs(cr[q] - sr[q]));
+                const double dl = sr[q] - cl[q], du = cu[q] - sr[q];
+                if (rtype[q] < R_NONE) rcm = fmax(rcm, fabs(cr[q] - sr[q]));
                 nz += fabs(zl[q]) + fabs(zu[q]);
-                if (hl[q]) comp0 = fmax(comp0, fabs(dl * zl[q]));
-                if (hu[q]) comp0 = fmax(comp0, fabs(du * zu[q]));
+                if (HL(q)) comp0 = fmax(comp0, fabs(dl * zl[q]));
+                if (HU(q)) comp0 = fmax(comp0, fabs(du * zu[q]));
             }
             ru = wmax(ru);
             rcm = wmax(rcm);
             nz = wsum(nz);
             comp0 = wmax(comp0);
-            const double sd = fmax(100.0, nz / (m_act + n)) / 100.0;
-            const double sc = fmax(100.0, nz / fmax(1.0, nbl)) / 100.0;
-            const double base_err = fmax(ru / sd, rcm);
-            e0 = fmax(base_err, comp0 / sc);
-            if (e0 <= P.tol) {
+            const double sd = uni(fmax(100.0, nz / (w.cst[K_MACT] + n)) / 100.0);
+            const double sc = uni(fmax(100.0, nz / fmax(1.0, w.cst[K_NBL])) / 100.0);
+            const double base_err = uni(fmax(ru / sd, rcm));
+            e0 = uni(fmax(base_err, comp0 / sc));
+            if (e0 <= w.cst[K_TOL]) {
                 status = 0;
                 break;
             }
-            if (it == P.max_iter) break;
-            const double mu_min = P.tol / 10.0;
+            if (it == max_iter) break;
+            const double mu_min = w.cst[K_TOL] / 10.0;
             const double mu_prev = mu;
             for (int t = 0; t < 8; ++t) {
                 double cm = 0.0;
 #pragma unroll
                 for (int q = 0; q < RPL; ++q) {
-                    const double dl = hl[q] ? sr[q] - cl[q] : 1.0, du = hu[q] ? cu[q] - sr[q] : 1.0;
-                    if (hl[q]) cm = fmax(cm, fabs(dl * zl[q] - mu));
-                    if (hu[q]) cm = fmax(cm, fabs(du * zu[q] - mu));
+                    const double dl = sr[q] - cl[q], du = cu[q] - sr[q];
+                    if (HL(q)) cm = fmax(cm, fabs(dl * zl[q] - mu));
+                    if (HU(q)) cm = fmax(cm, fabs(du * zu[q] - mu));
                 }
                 cm = wmax(cm);
                 if (fmax(base_err, cm / sc) <= 10.0 * mu && mu > mu_min)
-                    mu = fmax(mu_min, fmin(0.2 * mu, pow(mu, 1.5)));
+                    mu = uni(fmax(mu_min, fmin(0.2 * mu, mu * sqrt(mu))));
                 else
                     break;
             }
             if (mu != mu_prev) {
                 nf = 0;
-                if (P.modi) {
-                    eps = 0.1 * sqrt(mu);
+                if (modi) {
+                    // smoothing width follows mu: re-evaluate the f_en rows at the same V
+                    eps = uni(0.1 * sqrt(mu));
+#pragma unroll
+                    for (int q = 0; q < RPL; ++q) {
+                        double o[6];
+#pragma unroll
+                        for (int i = 0; i < 6; ++i) o[i] = w.obs6[6 * roi[q] + i];
+                        cr[q] = row_value(rtype[q], rk[q], rv[q], ra0[q], ra1[q], o, CK, eps);
+                    }
                     reeval = true;
                     continue;
                 }
@@ -926,50 +1239,76 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
             break;
         }
         STAMP(2);
-        if (status == 0 || it == P.max_iter) break;
-        const double tau = fmax(0.99, 1.0 - mu);
+        if (status == 0 || it == max_iter) break;
+        const double tau = uni(fmax(0.99, 1.0 - mu));
 
-        // ---- KKT: Sigma, w, Hessian blocks; K = J^T Sigma J + G^T S G by f64 MFMA
+        // ---- Sigma, rhs weights, Hessian blocks
+        RELANE();
         double rcv[RPL];
 #pragma unroll
         for (int q = 0; q < RPL; ++q) {
             const int r = lane + WAVE * q;
-            const double dl = hl[q] ? sr[q] - cl[q] : 1.0, du = hu[q] ? cu[q] - sr[q] : 1.0;
-            const double sg = (hl[q] ? zl[q] / dl : 0.0) + (hu[q] ? zu[q] / du : 0.0);
-            rcv[q] = cr[q] - sr[q];
-            if (r < P.mr4) {
+            const double sg = zl[q] * idl[q] + zu[q] * idu[q];
+            rcv[q] = rtype[q] < R_NONE ? cr[q] - sr[q] : 0.0;
+            double wr = mu * idl[q] - mu * idu[q] - sg * rcv[q];
+            wr = rtype[q] == R_OBJ ? -1.0 : wr;
+            if (r < mo4) {
                 w.rsig[r] = sg;
-                w.rw[r] = (hl[q] ? mu / dl : 0.0) - (hu[q] ? mu / du : 0.0) - sg * rcv[q];
+                w.rw[r] = wr;
             }
         }
-        STAMP(3);
-        hess_pass<N>(P, w, eps, gxg, gyg);
+        RELANE();
+        hess_blocks<N>(w, eps, lane, rps, nobs, modi);
         wave_sync();
+        STAMP(3);
+        // ---- K = J^T Sigma J + G^T S G by f64 MFMA (two accumulator chains), rhs = J^T w - grad f
         double rhsc[NT];
+        RELANE();
         {
-            d4 acc[NT * (NT + 1) / 2];
+            constexpr int NA = NT * (NT + 1) / 2;
+            d4 acc[2][NA];
 #pragma unroll
-            for (int i = 0; i < NT * (NT + 1) / 2; ++i) acc[i] = d4{0.0, 0.0, 0.0, 0.0};
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int i = 0; i < NA; ++i) acc[h][i] = d4{0.0, 0.0, 0.0, 0.0};
             double pw[NT];
 #pragma unroll
             for (int T = 0; T < NT; ++T) pw[T] = 0.0;
-            for (int s4 = 0; s4 < P.mr4; s4 += 4) {
-                const int r = s4 + g4;
-                const double sg = w.rsig[r], wr = w.rw[r];
-                double jv[NT];
 #pragma unroll
-                for (int T = 0; T < NT; ++T) {
-                    jv[T] = jrow_col(w.rcoef, w.rgen, G, NCP, r, 16 * T + col);
-                    pw[T] += jv[T] * wr;
-                }
-                acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(jv[0], sg * jv[0], acc[0], 0, 0, 0);
-                if constexpr (NT == 2) {
-                    acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(jv[0], sg * jv[1], acc[1], 0, 0, 0);
-                    acc[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(jv[1], sg * jv[1], acc[2], 0, 0, 0);
+            for (int s = 0; s < KSM; ++s) {
+                if (4 * s < mo4) {
+                    const int r = 4 * s + g4;
+                    const double sg = w.rsig[r], wr = w.rw[r];
+                    double j[NT];
+                    if constexpr (JC) {
+#pragma unroll
+                        for (int T = 0; T < NT; ++T) j[T] = jv[JC ? s : 0][T];
+                    } else {
+                        const uint32_t pk = w.rgen[r];
+                        const double2* rc2 = reinterpret_cast<const double2*>(w.rcoef + 4 * r);
+                        const double2 ca = rc2[0], cb = rc2[1];
+#pragma unroll
+                        for (int T = 0; T < NT; ++T) {
+                            const int cc = 16 * T + col;
+                            j[T] = ca.x * G[gen_i(pk, 0) * NCP + cc] + ca.y * G[gen_i(pk, 1) * NCP + cc] +
+                                   cb.x * G[gen_i(pk, 2) * NCP + cc] + cb.y * G[gen_i(pk, 3) * NCP + cc];
+                        }
+                    }
+#pragma unroll
+                    for (int T = 0; T < NT; ++T) pw[T] += j[T] * wr;
+                    if (4 * s < mr4) {
+                        d4* a = acc[s & 1];
+                        a[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(j[0], sg * j[0], a[0], 0, 0, 0);
+                        if constexpr (NT == 2) {
+                            a[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(j[0], sg * j[1], a[1], 0, 0, 0);
+                            a[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(j[1], sg * j[1], a[2], 0, 0, 0);
+                        }
+                    }
                 }
             }
-            for (int t0 = 4; t0 < NG; t0 += 4) {
-                const int t = t0 + g4;
+#pragma unroll
+            for (int s = 1; s < NG / 4; ++s) {
+                const int t = 4 * s + g4;
                 const int kb = t >> 3, c = t & 7;
                 const double* Srow = w.S + 64 * kb + 8 * c;
                 const double* Gb = G + 8 * kb * NCP;
@@ -982,29 +1321,32 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
                     for (int c2 = 0; c2 < 8; ++c2) a += Srow[c2] * Gb[c2 * NCP + 16 * T + col];
                     sgv[T] = a;
                 }
-                acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(gv[0], sgv[0], acc[0], 0, 0, 0);
+                d4* a = acc[s & 1];
+                a[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(gv[0], sgv[0], a[0], 0, 0, 0);
                 if constexpr (NT == 2) {
-                    acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(gv[0], sgv[1], acc[1], 0, 0, 0);
-                    acc[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(gv[1], sgv[1], acc[2], 0, 0, 0);
+                    a[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(gv[0], sgv[1], a[1], 0, 0, 0);
+                    a[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(gv[1], sgv[1], a[2], 0, 0, 0);
                 }
             }
 #pragma unroll
-            for (int T = 0; T < NT; ++T) rhsc[T] = gsum(pw[T]) - gfc[T];
+            for (int T = 0; T < NT; ++T) rhsc[T] = gsum(pw[T]);
             // C/D layout of v_mfma_f64_16x16x4: lane holds D[g4 + 4*i][col], i = 0..3
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int row = g4 + 4 * i;
-                w.K[row * KLD + col] = acc[0][i];
+                w.K[row * KLD + col] = acc[0][0][i] + acc[1][0][i];
                 if constexpr (NT == 2) {
-                    w.K[row * KLD + 16 + col] = acc[1][i];
-                    w.K[(16 + col) * KLD + row] = acc[1][i];
-                    w.K[(16 + row) * KLD + 16 + col] = acc[2][i];
+                    const double k1 = acc[0][1][i] + acc[1][1][i];
+                    w.K[row * KLD + 16 + col] = k1;
+                    w.K[(16 + col) * KLD + row] = k1;
+                    w.K[(16 + row) * KLD + 16 + col] = acc[0][2][i] + acc[1][2][i];
                 }
             }
         }
         wave_sync();
         STAMP(4);
-        // ---- factor with inertia correction, solve for du
+        // ---- factor with inertia correction, solve for dp
+        RELANE();
         double xv;
         {
             double rhs_l = 0.0;
@@ -1024,7 +1366,7 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
                     dw *= dw_last == 0.0 ? 100.0 : 8.0;
                     if (dw > 1e40) break;
                 }
-                dw_last = dw;
+                dw_last = uni(dw);
             }
             // forward: L y = rhs
             double acc = 0.0, yv = 0.0;
@@ -1051,104 +1393,101 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
             }
         }
         STAMP(5);
-        // ---- dV = G du  (du staged through LDS, read as broadcasts)
-        if (lane < n) w.Vt[lane] = xv;
-        wave_sync();
-        for (int t = lane; t < NG; t += WAVE) {
-            const double* gr = G + t * NCP;
+        // ---- dV = G dp (lane t), rows pick up their 4 entries
+        RELANE();
+        {
             double v = 0.0;
 #pragma unroll
-            for (int j = 0; j < n; ++j) v += gr[j] * w.Vt[j];
-            w.dV[t] = v;
+            for (int j = 0; j < n; ++j) v += G[(lane < NG ? lane : 0) * NCP + j] * bcast(xv, j);
+            dvme = lane < NG ? v : 0.0;
+            if (lane < NG) w.dV[lane] = dvme;
         }
         wave_sync();
         // ---- slack / multiplier steps, fraction to boundary
+        RELANE();
         double dS[RPL], dZl[RPL], dZu[RPL];
-        double ap = 1.0, az = 1.0, theta = 0.0, lsum = 0.0, sl = 0.0;
+        double ap = 1.0, az = 1.0, theta = 0.0, sl = 0.0, gdv = 0.0;
 #pragma unroll
         for (int q = 0; q < RPL; ++q) {
             const int r = lane + WAVE * q;
-            const double dl = hl[q] ? sr[q] - cl[q] : 1.0, du = hu[q] ? cu[q] - sr[q] : 1.0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) rdv[q][i] = w.dV[gen_i(rg[q], i)];
             double jd = 0.0;
-            if (r < P.mr4) {
-                const double* cf = w.rcoef + 4 * r;
-                const uint8_t* gn = w.rgen + 4 * r;
-                jd = cf[0] * w.dV[gn[0]] + cf[1] * w.dV[gn[1]] + cf[2] * w.dV[gn[2]] + cf[3] * w.dV[gn[3]];
+            if (r < mo4) {
+                const double2* rc2 = reinterpret_cast<const double2*>(w.rcoef + 4 * r);
+                const double2 ca = rc2[0], cb = rc2[1];
+                jd = ca.x * rdv[q][0] + ca.y * rdv[q][1] + cb.x * rdv[q][2] + cb.y * rdv[q][3];
             }
-            dS[q] = jd + rcv[q];
-            dZl[q] = hl[q] ? mu / dl - zl[q] - zl[q] / dl * dS[q] : 0.0;
-            dZu[q] = hu[q] ? mu / du - zu[q] + zu[q] / du * dS[q] : 0.0;
-            if (hl[q] && dS[q] < 0) ap = fmin(ap, -tau * dl / dS[q]);
-            if (hu[q] && dS[q] > 0) ap = fmin(ap, tau * du / dS[q]);
-            if (hl[q] && dZl[q] < 0) az = fmin(az, -tau * zl[q] / dZl[q]);
-            if (hu[q] && dZu[q] < 0) az = fmin(az, -tau * zu[q] / dZu[q]);
-            if (ri[q].type != R_NONE) theta += fabs(rcv[q]);
-            if (hl[q]) {
-                lsum += log(dl);
-                sl += dS[q] / dl;
-            }
-            if (hu[q]) {
-                lsum += log(du);
-                sl -= dS[q] / du;
-            }
+            if (rtype[q] == R_OBJ) gdv += jd;
+            dS[q] = rtype[q] < R_NONE ? jd + rcv[q] : 0.0;
+            dZl[q] = HL(q) ? mu * idl[q] - zl[q] - zl[q] * idl[q] * dS[q] : 0.0;
+            dZu[q] = HU(q) ? mu * idu[q] - zu[q] + zu[q] * idu[q] * dS[q] : 0.0;
+            const double dl = sr[q] - cl[q], du = cu[q] - sr[q];
+            if (HL(q) && dS[q] < 0) ap = fmin(ap, -tau * dl / dS[q]);
+            if (HU(q) && dS[q] > 0) ap = fmin(ap, tau * du / dS[q]);
+            if (HL(q) && dZl[q] < 0) az = fmin(az, -tau * zl[q] / dZl[q]);
+            if (HU(q) && dZu[q] < 0) az = fmin(az, -tau * zu[q] / dZu[q]);
+            theta += fabs(rcv[q]);
+            sl += (HL(q) ? dS[q] * idl[q] : 0.0) - (HU(q) ? dS[q] * idu[q] : 0.0);
         }
-        double gdv = lane < NG ? w.gfg[lane] * w.dV[lane] : 0.0;
         ap = wmin(ap);
         az = wmin(az);
-        wsum2(theta, lsum);
-        wsum2(sl, gdv);
-        const double phi = f - mu * lsum;
-        const double gphi = gdv - mu * sl;
+        wsum2(theta, gdv);
+        sl = wsum(sl);
+        const double phi = uni(f_cur - mu * lsum_cur);
+        const double gphi = uni(gdv - mu * sl);
+        const double pth = uni(pow(theta, sth));
+        const double pgp = uni(gphi < 0 ? pow(-gphi, sph) : 0.0);
         double amin;
         if (gphi < 0) {
             amin = fmin(gth, gph * theta / -gphi);
-            if (theta <= theta_min) amin = fmin(amin, pow(theta, sth) / pow(-gphi, sph));
+            if (theta <= w.cst[K_THMIN]) amin = fmin(amin, pth / pgp);
         } else {
             amin = gth;
         }
-        amin *= gal;
+        amin = uni(amin * gal);
         STAMP(6);
-        // ---- filter line search on trial points V + a dV
+        // ---- filter line search on trial points V + a dV (row registers only)
         double a = ap;
         bool accepted = false, ftype = false;
-        double ctr[RPL];
+        double ctr[RPL], ta0[RPL], ta1[RPL], vt[RPL][4];
+        double ft = 0.0, lgt = 0.0;
         while (a >= amin) {
-            for (int t = lane; t < NG; t += WAVE) w.Vt[t] = w.V[t] + a * w.dV[t];
-            wave_sync();
-            double fk = state_pass<N, false>(P, w.Vt, w.CT, w.ST, w.gfg, gxg, gyg);
-            wave_sync();
-            double tht = 0.0, lg = 0.0;
+            RELANE();
+            double tht = 0.0;
+            ft = 0.0;
+            lgt = 0.0;
             bool bad = false;
 #pragma unroll
             for (int q = 0; q < RPL; ++q) {
-                ctr[q] = row_eval<N, false>(P, ri[q], w.Vt, w.CT, w.ST, w.obs, eps, nullptr, nullptr);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) vt[q][i] = fma(a, rdv[q][i], rv[q][i]);
+                double o[6];
+#pragma unroll
+                for (int i = 0; i < 6; ++i) o[i] = w.obs6[6 * roi[q] + i];
+                row_trans(rtype[q], vt[q], w.cst[K_GXG], w.cst[K_GYG], ta0[q], ta1[q]);
+                ctr[q] = row_value(rtype[q], rk[q], vt[q], ta0[q], ta1[q], o, CK, eps);
                 const double st = sr[q] + a * dS[q];
-                if (ri[q].type != R_NONE) tht += fabs(ctr[q] - st);
-                if (hl[q]) {
-                    const double d = st - cl[q];
-                    if (!(d > 0)) bad = true;
-                    lg += log(d);
-                }
-                if (hu[q]) {
-                    const double d = cu[q] - st;
-                    if (!(d > 0)) bad = true;
-                    lg += log(d);
-                }
+                if (rtype[q] < R_NONE) tht += fabs(ctr[q] - st);
+                if (rtype[q] == R_OBJ) ft += ctr[q];
+                const double d1 = st - cl[q], d2 = cu[q] - st;
+                if (HL(q) && !(d1 > 0)) bad = true;
+                if (HU(q) && !(d2 > 0)) bad = true;
+                lgt += HL(q) ? (HU(q) ? log(d1 * d2) : log(d1)) : (HU(q) ? log(d2) : 0.0);
             }
-            double ft = fk;
             wsum2(ft, tht);
-            lg = wsum(lg);
+            lgt = wsum(lgt);
             const bool anybad = __ballot(bad) != 0ull;
-            const double pht = anybad ? INFINITY : ft - mu * lg;
-            bool ok = isfinite(pht) && tht < theta_max;
+            const double pht = anybad ? INFINITY : ft - mu * lgt;
+            bool ok = isfinite(pht) && tht < w.cst[K_THMAX];
             if (ok) {
                 const bool b0 = lane < nf && !(tht < fth0 || pht < fph0);
                 const bool b1 = lane + WAVE < nf && !(tht < fth1 || pht < fph1);
                 ok = __ballot(b0 || b1) == 0ull;
             }
             if (ok) {
-                const bool switching = gphi < 0 && a * pow(-gphi, sph) > pow(theta, sth);
-                if (switching && theta <= theta_min) {
+                const bool switching = gphi < 0 && a * pgp > pth;
+                if (switching && theta <= w.cst[K_THMIN]) {
                     if (pht <= phi + eta * a * gphi) {
                         accepted = true;
                         ftype = true;
@@ -1159,82 +1498,97 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
                 }
             }
             if (accepted) break;
-            a *= 0.5;
+            a = uni(a * 0.5);
         }
         STAMP(7);
+        RELANE();
         if (accepted) {
             if (!ftype && nf < FILTER_CAP) {
-                const double vt = (1 - gth) * theta, vp = phi - gph * theta;
+                const double fvt = (1 - gth) * theta, fvp = phi - gph * theta;
                 if ((nf & (WAVE - 1)) == lane) {
                     if (nf < WAVE) {
-                        fth0 = vt;
-                        fph0 = vp;
+                        fth0 = fvt;
+                        fph0 = fvp;
                     } else {
-                        fth1 = vt;
-                        fph1 = vp;
+                        fth1 = fvt;
+                        fph1 = fvp;
                     }
                 }
                 nf++;
             }
-            for (int t = lane; t < NG; t += WAVE) w.V[t] = w.Vt[t];
+            vme = fma(a, dvme, vme);
 #pragma unroll
             for (int q = 0; q < RPL; ++q) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) rv[q][i] = vt[q][i];
+                ra0[q] = ta0[q];
+                ra1[q] = ta1[q];
                 sr[q] += a * dS[q];
                 cr[q] = ctr[q];
             }
+            f_cur = ft;
+            lsum_cur = lgt;
         } else {
             // restoration substitute: shortest tried step, slacks reset onto c(u), filter reset
-            a = fmax(a, amin);
-            for (int t = lane; t < NG; t += WAVE) w.V[t] += a * w.dV[t];
-            wave_sync();
-            state_pass<N, false>(P, w.V, w.CT, w.ST, w.gfg, gxg, gyg);
-            wave_sync();
+            a = uni(fmax(a, amin));
+            vme = fma(a, dvme, vme);
+            double fr = 0.0, lr = 0.0;
 #pragma unroll
             for (int q = 0; q < RPL; ++q) {
-                cr[q] = row_eval<N, false>(P, ri[q], w.V, w.CT, w.ST, w.obs, eps, nullptr, nullptr);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) rv[q][i] = fma(a, rdv[q][i], rv[q][i]);
+                double o[6];
+#pragma unroll
+                for (int i = 0; i < 6; ++i) o[i] = w.obs6[6 * roi[q] + i];
+                row_trans(rtype[q], rv[q], w.cst[K_GXG], w.cst[K_GYG], ra0[q], ra1[q]);
+                cr[q] = row_value(rtype[q], rk[q], rv[q], ra0[q], ra1[q], o, CK, eps);
                 double v = cr[q];
-                const double pl = hl[q] ? fmin(1e-2 * fmax(1.0, fabs(cl[q])), 1e-2 * (cu[q] - cl[q])) : 0.0;
-                const double pu = hu[q] ? fmin(1e-2 * fmax(1.0, fabs(cu[q])), 1e-2 * (cu[q] - cl[q])) : 0.0;
-                if (hl[q] && hu[q])
+                const double pl = HL(q) ? fmin(1e-2 * fmax(1.0, fabs(cl[q])), 1e-2 * (cu[q] - cl[q])) : 0.0;
+                const double pu = HU(q) ? fmin(1e-2 * fmax(1.0, fabs(cu[q])), 1e-2 * (cu[q] - cl[q])) : 0.0;
+                if (HL(q) && HU(q))
                     v = fmin(fmax(v, cl[q] + pl), cu[q] - pu);
-                else if (hl[q])
+                else if (HL(q))
                     v = fmax(v, cl[q] + pl);
-                else if (hu[q])
+                else if (HU(q))
                     v = fmin(v, cu[q] - pu);
-                sr[q] = v;
+                sr[q] = rtype[q] < R_NONE ? v : 0.0;
+                const double d1 = sr[q] - cl[q], d2 = cu[q] - sr[q];
+                lr += HL(q) ? (HU(q) ? log(d1 * d2) : log(d1)) : (HU(q) ? log(d2) : 0.0);
+                if (rtype[q] == R_OBJ) fr += cr[q];
             }
+            wsum2(fr, lr);
+            f_cur = fr;
+            lsum_cur = lr;
             nf = 0;
             // infeasibility detection (stands in for IPOPT's failed restoration phase)
             n_rest++;
             double viol = 0.0;
 #pragma unroll
             for (int q = 0; q < RPL; ++q) {
-                if (hl[q]) viol = fmax(viol, clo[q] - cr[q]);
-                if (hu[q]) viol = fmax(viol, cr[q] - cuo[q]);
+                const int r = lane + WAVE * q;
+                if (r < mr4 && rtype[q] < R_NONE) {
+                    if (HL(q)) viol = fmax(viol, w.rclo[r] - cr[q]);
+                    if (HU(q)) viol = fmax(viol, cr[q] - w.rcuo[r]);
+                }
             }
             viol = wmax(viol);
             if (n_rest >= REST_FAIL && viol > 1e-4) {
+                if (lane < NG) w.V[lane] = vme;
                 status = 2;
                 it++;
                 break;
             }
         }
+        if (lane < NG) w.V[lane] = vme;
 #pragma unroll
         for (int q = 0; q < RPL; ++q) {
             zl[q] += az * dZl[q];
             zu[q] += az * dZu[q];
-            if (hl[q]) {
-                const double d = sr[q] - cl[q];
-                zl[q] = fmin(fmax(zl[q], mu / (1e10 * d)), 1e10 * mu / d);
-            } else {
-                zl[q] = 0.0;
-            }
-            if (hu[q]) {
-                const double d = cu[q] - sr[q];
-                zu[q] = fmin(fmax(zu[q], mu / (1e10 * d)), 1e10 * mu / d);
-            } else {
-                zu[q] = 0.0;
-            }
+            const double d1 = sr[q] - cl[q], d2 = cu[q] - sr[q];
+            idl[q] = HL(q) ? 1.0 / d1 : 0.0;
+            idu[q] = HU(q) ? 1.0 / d2 : 0.0;
+            zl[q] = HL(q) ? fmin(fmax(zl[q], mu * 1e-10 * idl[q]), 1e10 * mu * idl[q]) : 0.0;
+            zu[q] = HU(q) ? fmin(fmax(zu[q], mu * 1e-10 * idu[q]), 1e10 * mu * idu[q]) : 0.0;
         }
         wave_sync();
         STAMP(9);
@@ -1243,18 +1597,23 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
     STAMP_FLUSH;
     // ---- status + outputs (violation measured on the reference's exact |.|)
     wave_sync();
+    RELANE();
     if (status != 0 && status != 2) {
-        state_pass<N, false>(P, w.V, w.CT, w.ST, w.gfg, gxg, gyg);
-        wave_sync();
         double viol = 0.0;
 #pragma unroll
         for (int q = 0; q < RPL; ++q) {
-            const double c = row_eval<N, false>(P, ri[q], w.V, w.CT, w.ST, w.obs, 0.0, nullptr, nullptr);
-            if (hl[q]) viol = fmax(viol, clo[q] - c);
-            if (hu[q]) viol = fmax(viol, c - cuo[q]);
+            const int r = lane + WAVE * q;
+            double o[6];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) o[i] = w.obs6[6 * roi[q] + i];
+            const double c = row_value(rtype[q], rk[q], rv[q], ra0[q], ra1[q], o, CK, 0.0);
+            if (r < mr4 && rtype[q] < R_NONE) {
+                if (HL(q)) viol = fmax(viol, w.rclo[r] - c);
+                if (HU(q)) viol = fmax(viol, c - w.rcuo[r]);
+            }
         }
         viol = wmax(viol);
-        if (e0 <= P.acc_tol)
+        if (e0 <= w.cst[K_ACCTOL])
             status = 1;
         else if (viol > 1e-4)
             status = 2;
@@ -1267,6 +1626,10 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
         if (P.status) P.status[b] = status;
         if (P.iters) P.iters[b] = it;
     }
+#undef RELANE
+#undef CK
+#undef HL
+#undef HU
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1292,7 +1655,7 @@ __global__ __launch_bounds__(256, 4) void eval_kernel(KP Pv)
     for (int i = threadIdx.x; i < NG * 5; i += blockDim.x) E[i] = Pv.E[i];
     __syncthreads();
     const KP& P = *Ps;
-    const int wv = threadIdx.x / WAVE;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);   // wave-uniform (SGPR)
     const int lane = lane_id();
     const long long b = (long long)blockIdx.x * WAVES_PER_BLOCK + wv;
     if (b >= P.B) return;
@@ -1376,7 +1739,7 @@ using namespace alip;
 struct Handle {
     alipmpc_cfg cfg;
     int device = 0;
-    int N = 3, n = 9, NG = 32, NCP = 16, NCPU = 16, rps = 0, m_max = 0, mr4 = 0;
+    int N = 3, n = 9, NG = 32, NCP = 16, NCPU = 16, rps = 0, m_max = 0, mr4 = 0, mo4 = 0;
     double* dGp = nullptr;
     double* dEp = nullptr;
     double* dGu = nullptr;
@@ -1486,12 +1849,15 @@ size_t smem_bytes(const Handle* h, bool solve)
 {
     int wsd = 0;
     switch (h->N) {
-#define WSCASE(NN) \
-    case NN: wsd = ws_doubles<NN>(h->cfg.nc_max, h->cfg.ne_max, h->mr4); break;
+#define WSCASE(NN)                                                                                     \
+    case NN:                                                                                           \
+        wsd = solve ? wss_doubles<NN>(h->cfg.nc_max, h->cfg.ne_max, h->mr4, h->mo4)                    \
+                    : ws_doubles<NN>(h->cfg.nc_max, h->cfg.ne_max, h->mr4);                            \
+        break;
         WSCASE(1) WSCASE(2) WSCASE(3) WSCASE(4) WSCASE(5) WSCASE(6)
 #undef WSCASE
     }
-    const int e = h->NG * 5 + ((h->NG * 5) & 1);
+    const int e = solve ? ((h->NG * 5 + 3) & ~3) : h->NG * 5 + ((h->NG * 5) & 1);
     const int ncp = solve ? h->NCP : h->NCPU;
     return sizeof(double) * ((size_t)KP_DOUBLES + (size_t)h->NG * ncp + e + (size_t)WAVES_PER_BLOCK * wsd);
 }
@@ -1506,6 +1872,7 @@ KP make_kp(const Handle* h, long long B, bool solve)
     P.rps = h->rps;
     P.m_max = h->m_max;
     P.mr4 = h->mr4;
+    P.mo4 = h->mo4;
     P.modi = c.variant == ALIPMPC_VARIANT_MODI;
     P.max_iter = c.max_iter;
     P.select_obs = c.select_obs;
@@ -1538,13 +1905,19 @@ hipError_t launch_t(bool solve, const KP& P, size_t smem, hipStream_t st)
 {
     const unsigned grid = (unsigned)((P.B + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
     if (solve) {
-        if (P.mr4 <= WAVE) {
-            (void)hipFuncSetAttribute((const void*)solve_kernel<N, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-            hipLaunchKernelGGL((solve_kernel<N, 1>), dim3(grid), dim3(WAVE * WAVES_PER_BLOCK), smem, st, P);
-        } else {
-            (void)hipFuncSetAttribute((const void*)solve_kernel<N, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-            hipLaunchKernelGGL((solve_kernel<N, 2>), dim3(grid), dim3(WAVE * WAVES_PER_BLOCK), smem, st, P);
-        }
+        // KSM = 4-row steps of the J layout, the smallest compiled size covering mo4 rows
+        auto go = [&](auto kern) {
+            (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(WAVE * WAVES_PER_BLOCK), smem, st, P);
+        };
+        if (P.mo4 <= 32)
+            go(solve_kernel<N, 8>);
+        else if (P.mo4 <= 64)
+            go(solve_kernel<N, 16>);
+        else if (P.mo4 <= 128)
+            go(solve_kernel<N, 32>);
+        else
+            go(solve_kernel<N, 48>);
     } else {
         (void)hipFuncSetAttribute((const void*)eval_kernel<N>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
         hipLaunchKernelGGL(eval_kernel<N>, dim3(grid), dim3(WAVE * WAVES_PER_BLOCK), smem, st, P);
@@ -1679,7 +2052,8 @@ int alipmpc_create(const alipmpc_cfg* cfg, int device, void** handle)
     h->rps = alipmpc_rows_per_step(cfg);
     h->m_max = cfg->N * h->rps;
     h->mr4 = (h->m_max + 3) & ~3;
-    if (h->mr4 > MAX_ROWS) {
+    h->mo4 = h->mr4 + 4 * ((cfg->N + 3) / 4);   // + the objective pseudo-rows of the solve kernel
+    if (h->mr4 > MAX_ROWS || h->mo4 > MAX_ROWS + 64) {
         delete h;
         return ALIPMPC_EINVAL;
     }
