@@ -82,7 +82,9 @@ struct KP {
 
 constexpr int KP_DOUBLES = (int)((sizeof(KP) + 15) / 16 * 2);
 
-enum RowType { R_VBX = 0, R_VBY, R_CIR, R_ELP, R_LEG, R_DTH, R_FEN, R_NONE, R_OBJ };
+// R_FEN is the reference's f_en row (eval); in the solve layout (modi) it is the smooth half
+// vbx + s dth <= bvx_hi and R_FENM the other half vbx - s dth <= bvx_hi (see row_bounds)
+enum RowType { R_VBX = 0, R_VBY, R_CIR, R_ELP, R_LEG, R_DTH, R_FEN, R_FENM, R_NONE, R_OBJ };
 
 // ---- diagnostic phase timers (compiled only with -DALIP_STAMPS; never in the product build)
 #ifdef ALIP_STAMPS
@@ -311,18 +313,28 @@ __device__ __forceinline__ RowInfo decode_row(const KP& P, int r, int nc_sel, in
         ri.type = R_LEG;
     } else if (l == 3 + P.nc_max + P.ne_max) {
         ri.type = R_DTH;
-    } else {
+    } else if (l == 4 + P.nc_max + P.ne_max) {
         ri.type = R_FEN;
+    } else {
+        ri.type = R_FENM;   // solve layout only
     }
     return ri;
 }
 
-__device__ __forceinline__ void row_bounds(const KP& P, const RowInfo& ri, int leg, double& cl, double& cu)
+// split (solve layout, modi): f_en = vbx + s|dth| in [bvx_lo, bvx_hi] becomes vbx +- s dth <= bvx_hi — the
+// same feasible set (|x| <= c <=> +-x <= c; the lower bound is implied by the vbx row since s > 0), but
+// smooth, so Newton steps are not trapped at the kink dth = 0.
+__device__ __forceinline__ void row_bounds(const KP& P, const RowInfo& ri, int leg, double& cl, double& cu,
+                                           bool split = false)
 {
     switch (ri.type) {
     case R_VBX:
-    case R_FEN:
         cl = P.bvx_lo;
+        cu = P.bvx_hi;
+        break;
+    case R_FEN:
+    case R_FENM:
+        cl = split ? -INFINITY : P.bvx_lo;
         cu = P.bvx_hi;
         break;
     case R_VBY: {
@@ -746,6 +758,7 @@ __device__ __forceinline__ uint32_t row_gens(int type, int k)
     case R_VBX:
     case R_VBY:
     case R_FEN:
+    case R_FENM:
         g0 = gx(k + 1, 2); g1 = gx(k + 1, 3); g2 = gx(k + 1, 4); g3 = gp(k, 2);
         break;
     case R_CIR:
@@ -795,14 +808,13 @@ __device__ __forceinline__ RowK load_rowk(const double* cst)
 
 // value of row `type` at generator values v (branch-free: every family is computed, one is selected)
 __device__ __forceinline__ double row_value(int type, int k, const double (&v)[4], double a0, double a1,
-                                            const double (&o)[6], const RowK& C, double eps)
+                                            const double (&o)[6], const RowK& C)
 {
-    // velocity family
+    // velocity family (f_en halves: vbx +- s dth)
     const bool vby = type == R_VBY;
     const double ca = vby ? -a0 : a1, cb = vby ? a1 : a0;
-    double fa, fd1, fd2;
-    sabs(v[3], eps, fa, fd1, fd2);
-    const double cvel = ca * v[0] + cb * v[1] + (type == R_FEN ? C.s * fa : 0.0);
+    const double sd = type == R_FEN ? C.s : (type == R_FENM ? -C.s : 0.0);
+    const double cvel = ca * v[0] + cb * v[1] + sd * v[3];
     // D-CBF (circle == ellipse with qa = qc = 1, qb = 0, ek = r^2)
     const double x1 = v[0] - o[0], y1 = v[1] - o[1], x0 = v[2] - o[0], y0 = v[3] - o[1];
     const double h1 = o[2] * x1 * x1 + o[3] * x1 * y1 + o[4] * y1 * y1 - o[5];
@@ -816,7 +828,7 @@ __device__ __forceinline__ double row_value(int type, int k, const double (&v)[4
     const double dxg = C.gxg - v[0], dyg = C.gyg - v[1];
     const double cobj = w * (dxg * dxg + dyg * dyg) + C.r * a0 * a0;
     double c = 0.0;
-    c = (type == R_VBX || vby || type == R_FEN) ? cvel : c;
+    c = (type == R_VBX || vby || type == R_FEN || type == R_FENM) ? cvel : c;
     c = (type == R_CIR || type == R_ELP) ? cobs : c;
     c = type == R_LEG ? cleg : c;
     c = type == R_DTH ? v[3] : c;
@@ -827,16 +839,13 @@ __device__ __forceinline__ double row_value(int type, int k, const double (&v)[4
 // generator-form gradient coefficients of row `type` (OBJ rows: grad f_k; hx = its 6 Hessian parts
 // [h00 h01 h11 h04 h14 h44] on (px, py, theta) of x_k)
 __device__ __forceinline__ void row_coef(int type, int k, const double (&v)[4], double a0, double a1,
-                                         const double (&o)[6], const RowK& C, double eps, double (&cf)[4],
-                                         double (&hx)[6])
+                                         const double (&o)[6], const RowK& C, double (&cf)[4], double (&hx)[6])
 {
-    const bool vby = type == R_VBY, vel = type == R_VBX || vby || type == R_FEN;
+    const bool vby = type == R_VBY, vel = type == R_VBX || vby || type == R_FEN || type == R_FENM;
     const bool obs = type == R_CIR || type == R_ELP;
     // velocity family: d/dtheta of (ca, cb)
     const double ca = vby ? -a0 : a1, cb = vby ? a1 : a0;
     const double da = vby ? -a1 : -a0, db = vby ? -a0 : a1;
-    double fa, fd1, fd2;
-    sabs(v[3], eps, fa, fd1, fd2);
     // D-CBF
     const double x1 = v[0] - o[0], y1 = v[1] - o[1], x0 = v[2] - o[0], y0 = v[3] - o[1];
     // leg
@@ -848,7 +857,7 @@ __device__ __forceinline__ void row_coef(int type, int k, const double (&v)[4], 
     const double gp0 = -dyg * ir2, gp1 = dxg * ir2, phi = a0;
     double c0 = 0.0, c1 = 0.0, c2 = 0.0, c3 = 0.0;
     if (vel) {
-        c0 = ca; c1 = cb; c2 = da * v[0] + db * v[1]; c3 = type == R_FEN ? C.s * fd1 : 0.0;
+        c0 = ca; c1 = cb; c2 = da * v[0] + db * v[1]; c3 = type == R_FEN ? C.s : (type == R_FENM ? -C.s : 0.0);
     }
     if (obs) {
         c0 = 2 * o[2] * x1 + o[3] * y1; c1 = 2 * o[4] * y1 + o[3] * x1;
@@ -879,13 +888,13 @@ __device__ __forceinline__ void row_coef(int type, int k, const double (&v)[4], 
 // come from the OBJ rows (hobj), everything else from y and the obstacle forms.
 // ------------------------------------------------------------------------------------------------
 template <int N>
-__device__ void hess_blocks(const WSS<N>& w, double eps, int lane, int rps, int nobs, int modi)
+__device__ void hess_blocks(const WSS<N>& w, int lane, int rps, int nobs, int modi)
 {
     if (lane > N) return;
-    const double gm1 = w.cst[K_GM1], s_fen = w.cst[K_S];
+    const double gm1 = w.cst[K_GM1];
     const int kb = lane;
     double h00 = 0, h01 = 0, h11 = 0, h04 = 0, h14 = 0, h44 = 0, h24 = 0, h34 = 0;
-    double h05 = 0, h55 = 0, h77 = 0;
+    double h05 = 0, h55 = 0;
     if (kb >= 1) {
         const double* ho = w.hobj + 6 * kb;
         h00 = ho[0]; h01 = ho[1]; h11 = ho[2]; h04 = ho[3]; h14 = ho[4]; h44 = ho[5];
@@ -894,7 +903,7 @@ __device__ void hess_blocks(const WSS<N>& w, double eps, int lane, int rps, int 
         const double ct = w.CT[kb], st = w.ST[kb];
         const double vx = w.V[gx(kb, 2)], vy = w.V[gx(kb, 3)];
         const double vbx = ct * vx + st * vy, vby = -st * vx + ct * vy;
-        const double wbx = w.ry[base + 0] + (modi ? w.ry[base + rps - 1] : 0.0);
+        const double wbx = w.ry[base + 0] + (modi ? w.ry[base + rps - 2] + w.ry[base + rps - 1] : 0.0);
         const double wby = w.ry[base + 1];
         h24 = wbx * st + wby * ct;
         h34 = -wbx * ct + wby * st;
@@ -926,18 +935,13 @@ __device__ void hess_blocks(const WSS<N>& w, double eps, int lane, int rps, int 
         h11 -= 2 * yl;
         h05 = 2 * yl;
         h55 = -2 * yl;
-        if (modi && eps != 0.0) {
-            double a, d1, d2;
-            sabs(w.V[gp(kb, 2)], eps, a, d1, d2);
-            h77 = -w.ry[base + rps - 1] * s_fen * d2;
-        }
     }
     double* S = w.S + 64 * kb;
     S[0 * 8 + 0] = h00; S[0 * 8 + 1] = h01; S[1 * 8 + 0] = h01; S[1 * 8 + 1] = h11;
     S[0 * 8 + 4] = h04; S[4 * 8 + 0] = h04; S[1 * 8 + 4] = h14; S[4 * 8 + 1] = h14;
     S[2 * 8 + 4] = h24; S[4 * 8 + 2] = h24; S[3 * 8 + 4] = h34; S[4 * 8 + 3] = h34; S[4 * 8 + 4] = h44;
     S[0 * 8 + 5] = h05; S[5 * 8 + 0] = h05; S[1 * 8 + 6] = h05; S[6 * 8 + 1] = h05;
-    S[5 * 8 + 5] = h55; S[6 * 8 + 6] = h55; S[7 * 8 + 7] = h77;
+    S[5 * 8 + 5] = h55; S[6 * 8 + 6] = h55;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1038,7 +1042,6 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
     double cl[RPL], cu[RPL], rv[RPL][4], rdv[RPL][4], ra0[RPL], ra1[RPL];
     double cr[RPL], sr[RPL], zl[RPL], zu[RPL], idl[RPL], idu[RPL];
     double mu = uni(P.mu_init);
-    double eps = modi ? 0.1 * sqrt(mu) : 0.0;
     double vme = lane < NG ? w.V[lane] : 0.0, dvme = 0.0;   // lane t's generator value / step
     double th0 = 0.0, nbl = 0.0, mal = 0.0, fo = 0.0, lg0 = 0.0;
     wave_sync();
@@ -1059,7 +1062,7 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
         rg[q] = row_gens(ri.type, ri.k);
         if (r < mo4) w.rgen[r] = rg[q];
         double clo, cuo;
-        row_bounds(P, ri, legv, clo, cuo);
+        row_bounds(P, ri, legv, clo, cuo, modi != 0);
         if (r < mr4) {
             w.rclo[r] = clo;
             w.rcuo[r] = cuo;
@@ -1077,7 +1080,7 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
 #pragma unroll
         for (int i = 0; i < 6; ++i) o[i] = w.obs6[6 * roi[q] + i];
         row_trans(rtype[q], rv[q], w.cst[K_GXG], w.cst[K_GYG], ra0[q], ra1[q]);
-        cr[q] = row_value(rtype[q], rk[q], rv[q], ra0[q], ra1[q], o, CK, eps);
+        cr[q] = row_value(rtype[q], rk[q], rv[q], ra0[q], ra1[q], o, CK);
         double v = cr[q];
         const double pl = HL(q) ? fmin(1e-2 * fmax(1.0, fabs(cl[q])), 1e-2 * (cu[q] - cl[q])) : 0.0;
         const double pu = HU(q) ? fmin(1e-2 * fmax(1.0, fabs(cu[q])), 1e-2 * (cu[q] - cl[q])) : 0.0;
@@ -1119,7 +1122,6 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
     for (it = 0; it <= max_iter; ++it) {
         double gl[NT];                                  // J^T y - grad f  (per column, all lanes)
         double jv[JC ? KSM : 1][NT];
-        bool reeval = false;
         for (;;) {
             RELANE();
             // ---- row layout: generator-form coefficients at V (OBJ rows: grad f_k and its Hessian parts)
@@ -1129,7 +1131,7 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
                 double o[6], cf[4], hx[6];
 #pragma unroll
                 for (int i = 0; i < 6; ++i) o[i] = w.obs6[6 * roi[q] + i];
-                row_coef(rtype[q], rk[q], rv[q], ra0[q], ra1[q], o, CK, eps, cf, hx);
+                row_coef(rtype[q], rk[q], rv[q], ra0[q], ra1[q], o, CK, cf, hx);
                 if (r < mo4) {
                     double2* rc2 = reinterpret_cast<double2*>(w.rcoef + 4 * r);
                     rc2[0] = make_double2(cf[0], cf[1]);
@@ -1175,7 +1177,6 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
 #pragma unroll
             for (int T = 0; T < NT; ++T) gl[T] = gsum(gl[T]);
             STAMP(1);
-            if (reeval) break;
             // ---- convergence test (IPOPT scaled overall error) and barrier update
             RELANE();
             double ru = 0.0;
@@ -1220,22 +1221,7 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
                 else
                     break;
             }
-            if (mu != mu_prev) {
-                nf = 0;
-                if (modi) {
-                    // smoothing width follows mu: re-evaluate the f_en rows at the same V
-                    eps = uni(0.1 * sqrt(mu));
-#pragma unroll
-                    for (int q = 0; q < RPL; ++q) {
-                        double o[6];
-#pragma unroll
-                        for (int i = 0; i < 6; ++i) o[i] = w.obs6[6 * roi[q] + i];
-                        cr[q] = row_value(rtype[q], rk[q], rv[q], ra0[q], ra1[q], o, CK, eps);
-                    }
-                    reeval = true;
-                    continue;
-                }
-            }
+            if (mu != mu_prev) nf = 0;
             break;
         }
         STAMP(2);
@@ -1258,7 +1244,7 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
             }
         }
         RELANE();
-        hess_blocks<N>(w, eps, lane, rps, nobs, modi);
+        hess_blocks<N>(w, lane, rps, nobs, modi);
         wave_sync();
         STAMP(3);
         // ---- K = J^T Sigma J + G^T S G by f64 MFMA (two accumulator chains), rhs = J^T w - grad f
@@ -1466,7 +1452,7 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
 #pragma unroll
                 for (int i = 0; i < 6; ++i) o[i] = w.obs6[6 * roi[q] + i];
                 row_trans(rtype[q], vt[q], w.cst[K_GXG], w.cst[K_GYG], ta0[q], ta1[q]);
-                ctr[q] = row_value(rtype[q], rk[q], vt[q], ta0[q], ta1[q], o, CK, eps);
+                ctr[q] = row_value(rtype[q], rk[q], vt[q], ta0[q], ta1[q], o, CK);
                 const double st = sr[q] + a * dS[q];
                 if (rtype[q] < R_NONE) tht += fabs(ctr[q] - st);
                 if (rtype[q] == R_OBJ) ft += ctr[q];
@@ -1541,7 +1527,7 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
 #pragma unroll
                 for (int i = 0; i < 6; ++i) o[i] = w.obs6[6 * roi[q] + i];
                 row_trans(rtype[q], rv[q], w.cst[K_GXG], w.cst[K_GYG], ra0[q], ra1[q]);
-                cr[q] = row_value(rtype[q], rk[q], rv[q], ra0[q], ra1[q], o, CK, eps);
+                cr[q] = row_value(rtype[q], rk[q], rv[q], ra0[q], ra1[q], o, CK);
                 double v = cr[q];
                 const double pl = HL(q) ? fmin(1e-2 * fmax(1.0, fabs(cl[q])), 1e-2 * (cu[q] - cl[q])) : 0.0;
                 const double pu = HU(q) ? fmin(1e-2 * fmax(1.0, fabs(cu[q])), 1e-2 * (cu[q] - cl[q])) : 0.0;
@@ -1606,7 +1592,7 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
             double o[6];
 #pragma unroll
             for (int i = 0; i < 6; ++i) o[i] = w.obs6[6 * roi[q] + i];
-            const double c = row_value(rtype[q], rk[q], rv[q], ra0[q], ra1[q], o, CK, 0.0);
+            const double c = row_value(rtype[q], rk[q], rv[q], ra0[q], ra1[q], o, CK);
             if (r < mr4 && rtype[q] < R_NONE) {
                 if (HL(q)) viol = fmax(viol, w.rclo[r] - c);
                 if (HU(q)) viol = fmax(viol, c - w.rcuo[r]);
@@ -1739,7 +1725,8 @@ using namespace alip;
 struct Handle {
     alipmpc_cfg cfg;
     int device = 0;
-    int N = 3, n = 9, NG = 32, NCP = 16, NCPU = 16, rps = 0, m_max = 0, mr4 = 0, mo4 = 0;
+    int N = 3, n = 9, NG = 32, NCP = 16, NCPU = 16, rps = 0, m_max = 0, mr4 = 0;
+    int rps_s = 0, m_s = 0, mr4_s = 0, mo4 = 0;   // solve-kernel row layout (f_en split, objective rows)
     double* dGp = nullptr;
     double* dEp = nullptr;
     double* dGu = nullptr;
@@ -1851,7 +1838,7 @@ size_t smem_bytes(const Handle* h, bool solve)
     switch (h->N) {
 #define WSCASE(NN)                                                                                     \
     case NN:                                                                                           \
-        wsd = solve ? wss_doubles<NN>(h->cfg.nc_max, h->cfg.ne_max, h->mr4, h->mo4)                    \
+        wsd = solve ? wss_doubles<NN>(h->cfg.nc_max, h->cfg.ne_max, h->mr4_s, h->mo4)                  \
                     : ws_doubles<NN>(h->cfg.nc_max, h->cfg.ne_max, h->mr4);                            \
         break;
         WSCASE(1) WSCASE(2) WSCASE(3) WSCASE(4) WSCASE(5) WSCASE(6)
@@ -1869,9 +1856,9 @@ KP make_kp(const Handle* h, long long B, bool solve)
     std::memset(&P, 0, sizeof(P));
     P.nc_max = c.nc_max;
     P.ne_max = c.ne_max;
-    P.rps = h->rps;
-    P.m_max = h->m_max;
-    P.mr4 = h->mr4;
+    P.rps = solve ? h->rps_s : h->rps;
+    P.m_max = solve ? h->m_s : h->m_max;
+    P.mr4 = solve ? h->mr4_s : h->mr4;
     P.mo4 = h->mo4;
     P.modi = c.variant == ALIPMPC_VARIANT_MODI;
     P.max_iter = c.max_iter;
@@ -1912,8 +1899,14 @@ hipError_t launch_t(bool solve, const KP& P, size_t smem, hipStream_t st)
         };
         if (P.mo4 <= 32)
             go(solve_kernel<N, 8>);
+        else if (P.mo4 <= 40)
+            go(solve_kernel<N, 10>);
+        else if (P.mo4 <= 48)
+            go(solve_kernel<N, 12>);
         else if (P.mo4 <= 64)
             go(solve_kernel<N, 16>);
+        else if (P.mo4 <= 96)
+            go(solve_kernel<N, 24>);
         else if (P.mo4 <= 128)
             go(solve_kernel<N, 32>);
         else
@@ -2052,7 +2045,10 @@ int alipmpc_create(const alipmpc_cfg* cfg, int device, void** handle)
     h->rps = alipmpc_rows_per_step(cfg);
     h->m_max = cfg->N * h->rps;
     h->mr4 = (h->m_max + 3) & ~3;
-    h->mo4 = h->mr4 + 4 * ((cfg->N + 3) / 4);   // + the objective pseudo-rows of the solve kernel
+    h->rps_s = h->rps + (cfg->variant == ALIPMPC_VARIANT_MODI ? 1 : 0);   // f_en -> two smooth rows
+    h->m_s = cfg->N * h->rps_s;
+    h->mr4_s = (h->m_s + 3) & ~3;
+    h->mo4 = h->mr4_s + 4 * ((cfg->N + 3) / 4);   // + the objective pseudo-rows of the solve kernel
     if (h->mr4 > MAX_ROWS || h->mo4 > MAX_ROWS + 64) {
         delete h;
         return ALIPMPC_EINVAL;

@@ -28,7 +28,7 @@
 #define OMAXN 8
 #define OMAXV (5 * OMAXN)
 #define OMAXO ALIPMPC_MAX_OBS
-#define OMAXM (OMAXN * (5 + OMAXO))
+#define OMAXM (OMAXN * (6 + OMAXO))
 
 typedef struct {
     int N, n;
@@ -45,12 +45,12 @@ typedef struct {
     const alipmpc_cfg* cfg;
     const oconsts* K;
     int N, n, m, rpk, nc, ne, modi;
+    int split;   /* solver-internal: f_en row replaced by the two smooth rows vbx +- s dth <= bvx_hi */
     double x0[5], goal[2], goal_orig[2];
     double cir[OMAXO][3], elp[OMAXO][5];
     double eqa[OMAXO], eqb[OMAXO], eqc[OMAXO], ek[OMAXO];
     int sel_c[OMAXO], sel_e[OMAXO];
     double cl[OMAXM], cu[OMAXM];
-    double eps_abs;
 } oprob;
 
 /* ------------------------------------------------------------------------------------------------ */
@@ -184,7 +184,7 @@ void oracle_consts(const alipmpc_cfg* cfg, oconsts* K)
 /* ------------------------------------------------------------------------------------------------ */
 /* set-up: select_obs, detour goal, cl/cu (compact reference row order) */
 static void oprob_init(oprob* P, const alipmpc_cfg* cfg, const oconsts* K, const double* x0, const double* goal,
-                       int leg, const double* cir, int nc, const double* elp, int ne)
+                       int leg, const double* cir, int nc, const double* elp, int ne, int split)
 {
     memset(P, 0, sizeof(*P));
     P->cfg = cfg;
@@ -192,6 +192,7 @@ static void oprob_init(oprob* P, const alipmpc_cfg* cfg, const oconsts* K, const
     P->N = cfg->N;
     P->n = 5 * cfg->N;
     P->modi = cfg->variant == ALIPMPC_VARIANT_MODI;
+    P->split = split && P->modi;
     memcpy(P->x0, x0, 5 * sizeof(double));
     P->goal_orig[0] = goal[0];
     P->goal_orig[1] = goal[1];
@@ -247,7 +248,7 @@ static void oprob_init(oprob* P, const alipmpc_cfg* cfg, const oconsts* K, const
         }
     }
     /* cl / cu (MPC_LIP_modi.py:205-245) */
-    P->rpk = 4 + P->nc + P->ne + P->modi;
+    P->rpk = 4 + P->nc + P->ne + P->modi + P->split;
     P->m = P->N * P->rpk;
     int r = 0;
     for (int k = 0; k < P->N; ++k) {
@@ -266,7 +267,13 @@ static void oprob_init(oprob* P, const alipmpc_cfg* cfg, const oconsts* K, const
         P->cu[r++] = cfg->leg2_max;
         P->cl[r] = -cfg->dtheta_max;
         P->cu[r++] = cfg->dtheta_max;
-        if (P->modi) {
+        if (P->split) {
+            /* |x| <= c  <=>  x <= c and -x <= c; the f_en lower bound is implied by the vbx row (s > 0) */
+            P->cl[r] = -INFINITY;
+            P->cu[r++] = cfg->bvx_hi;
+            P->cl[r] = -INFINITY;
+            P->cu[r++] = cfg->bvx_hi;
+        } else if (P->modi) {
             P->cl[r] = cfg->bvx_lo;
             P->cu[r++] = cfg->bvx_hi;
         }
@@ -303,16 +310,10 @@ static void rollout(const oprob* P, const double* u, double X[][5], double Pp[][
 
 static void oabs(const oprob* P, double x, double* v, double* d1, double* d2)
 {
-    if (P->eps_abs == 0.0) {
-        *v = fabs(x);
-        *d1 = x == 0 ? 0.0 : copysign(1.0, x);
-        *d2 = 0.0;
-    } else {
-        double r = sqrt(x * x + P->eps_abs * P->eps_abs);
-        *v = r;
-        *d1 = x / r;
-        *d2 = P->eps_abs * P->eps_abs / (r * r * r);
-    }
+    (void)P;   /* |x| with the reference's derivative sign(x) (MPC_LIP_modi.py:637-643) */
+    *v = fabs(x);
+    *d1 = x == 0 ? 0.0 : copysign(1.0, x);
+    *d2 = 0.0;
 }
 
 static double h_obs(const oprob* P, int j, double px, double py)
@@ -392,7 +393,10 @@ static void constraints(const oprob* P, const double* u, double* out)
         for (int j = 0; j < P->nc + P->ne; ++j) out[r++] = h_obs(P, j, X[i + 1][0], X[i + 1][1]) + gm1 * h_obs(P, j, X[i][0], X[i][1]);
         out[r++] = (X[i][0] - Pp[i][0]) * (X[i][0] - Pp[i][0]) + (X[i][1] - Pp[i][1]) * (X[i][1] - Pp[i][1]);
         out[r++] = Pp[i][2];
-        if (P->modi) {
+        if (P->split) {
+            out[r++] = vbx + c->s * Pp[i][2];
+            out[r++] = vbx - c->s * Pp[i][2];
+        } else if (P->modi) {
             double a, d1, d2;
             oabs(P, Pp[i][2], &a, &d1, &d2);
             out[r++] = c->s * a + vbx;
@@ -432,7 +436,12 @@ static void jacobian(const oprob* P, const double* u, double* J /* m x n */)
         r++;
         for (int j = 0; j < n; ++j) J[(size_t)r * n + j] = Ps[2][j];
         r++;
-        if (P->modi) {
+        if (P->split) {
+            for (int j = 0; j < n; ++j) J[(size_t)r * n + j] = rbx[j] + c->s * Ps[2][j];
+            r++;
+            for (int j = 0; j < n; ++j) J[(size_t)r * n + j] = rbx[j] - c->s * Ps[2][j];
+            r++;
+        } else if (P->modi) {
             double a, d1, d2;
             oabs(P, Pp[i][2], &a, &d1, &d2);
             for (int j = 0; j < n; ++j) J[(size_t)r * n + j] = c->s * d1 * Ps[2][j] + rbx[j];
@@ -476,7 +485,7 @@ static void hessian(const oprob* P, const double* u, const double* y, double* H 
         const double* yk = y + i * P->rpk;
         double th = X[i + 1][4], vx = X[i + 1][2], vy = X[i + 1][3], ct = cos(th), st = sin(th);
         double vbx = ct * vx + st * vy, vby = -st * vx + ct * vy;
-        double wbx = yk[0] + (P->modi ? yk[P->rpk - 1] : 0.0), wby = yk[1];
+        double wbx = yk[0] + (P->split ? yk[P->rpk - 2] + yk[P->rpk - 1] : P->modi ? yk[P->rpk - 1] : 0.0), wby = yk[1];
         double hvx = -wbx * (-st) - wby * (-ct);
         double hvy = -wbx * ct - wby * (-st);
         Hl[i + 1][2][4] += hvx;
@@ -516,7 +525,7 @@ static void hessian(const oprob* P, const double* u, const double* y, double* H 
                 H[a * n + b] += -wl * 2 * (e0a * e0b + e1a * e1b);
             }
         }
-        if (P->modi) {
+        if (P->modi && !P->split) {
             double av, d1, d2;
             oabs(P, Pp[i][2], &av, &d1, &d2);
             if (d2 != 0.0) {
@@ -593,7 +602,6 @@ static void push_slacks(const double* c, const double* cl, const double* cu, int
     }
 }
 
-static double eps_abs_of_mu(double mu) { return 0.1 * sqrt(mu); }
 
 static double barrier(double f, const double* s, const double* cl, const double* cu, int m, double mu)
 {
@@ -698,7 +706,6 @@ static void osolve(oprob* P, const double* u0, double* uout, osolve_info* info)
     const alipmpc_cfg* cfg = P->cfg;
     const int n = 3 * P->N, m = P->m;
     double u[OMAXV];   /* the decision: footholds p (n = 3N) */
-    const int smooth = P->modi;
     double cl[OMAXM], cu[OMAXM];
     int hl[OMAXM], hu[OMAXM];
     int nb = 0;
@@ -716,7 +723,6 @@ static void osolve(oprob* P, const double* u0, double* uout, osolve_info* info)
             for (int c = 0; c < 3; ++c) u[3 * k + c] = Pp0[k][c];
     }
     double mu = cfg->mu_init;
-    P->eps_abs = smooth ? eps_abs_of_mu(mu) : 0.0;
     double c[OMAXM], s[OMAXM], zl[OMAXM], zu[OMAXM];
     pcons(P, u, c);
     push_slacks(c, cl, cu, m, s);
@@ -777,21 +783,11 @@ static void osolve(oprob* P, const double* u0, double* uout, osolve_info* info)
         double mu_min = cfg->tol / 10.0, mu_old = mu;
         for (int t = 0; t < 8; ++t) {
             if (ERR(mu) <= 10.0 * mu && mu > mu_min)
-                mu = fmax(mu_min, fmin(0.2 * mu, pow(mu, 1.5)));
+                mu = fmax(mu_min, fmin(0.2 * mu, mu * sqrt(mu)));
             else
                 break;
         }
-        if (mu != mu_old) {
-            nf = 0;
-            if (smooth) {
-                P->eps_abs = eps_abs_of_mu(mu);
-                f = pobj(P, u);
-                pgrad(P, u, gf);
-                pjac(P, u, J);
-                pcons(P, u, c);
-                for (int i = 0; i < m; ++i) rc[i] = c[i] - s[i];
-            }
-        }
+        if (mu != mu_old) nf = 0;
         double tau = fmax(0.99, 1.0 - mu);
         for (int i = 0; i < m; ++i) Sig[i] = (hl[i] ? zl[i] / dl[i] : 0.0) + (hu[i] ? zu[i] / du[i] : 0.0);
         phess(P, u, y, H);
@@ -930,7 +926,6 @@ static void osolve(oprob* P, const double* u0, double* uout, osolve_info* info)
 #undef ERR
     }
     free(ft);
-    P->eps_abs = 0.0;
     if (status != 0 && status != 2) {
         pcons(P, u, c);
         double viol = 0;
@@ -969,7 +964,7 @@ int oracle_solve_batch(const alipmpc_cfg* cfg, int64_t B, const double* x0, cons
     for (int64_t b = 0; b < B; ++b) {
         oprob* P = (oprob*)malloc(sizeof(oprob));
         oprob_init(P, cfg, K, x0 + 5 * b, goal + 2 * b, leg[b], cir + (size_t)3 * cfg->nc_max * b, nc[b],
-                   elp ? elp + (size_t)5 * cfg->ne_max * b : NULL, ne ? ne[b] : 0);
+                   elp ? elp + (size_t)5 * cfg->ne_max * b : NULL, ne ? ne[b] : 0, 1);
         double u[OMAXV];
         osolve_info info;
         osolve(P, u0 + (size_t)n * b, u, &info);
@@ -1003,7 +998,7 @@ int oracle_eval_batch(const alipmpc_cfg* cfg, int64_t B, const double* x0, const
     double cc[OMAXM];
     for (int64_t b = 0; b < B; ++b) {
         oprob_init(P, cfg, K, x0 + 5 * b, goal + 2 * b, leg[b], cir + (size_t)3 * cfg->nc_max * b, nc[b],
-                   elp ? elp + (size_t)5 * cfg->ne_max * b : NULL, ne ? ne[b] : 0);
+                   elp ? elp + (size_t)5 * cfg->ne_max * b : NULL, ne ? ne[b] : 0, 0);
         const double* ub = u + (size_t)n * b;
         if (f) f[b] = oracle_objective(P, ub);
         if (grad) gradient(P, ub, grad + (size_t)n * b);
