@@ -660,6 +660,25 @@ __device__ void prologue(const KP& P, const WT& w, const double* G, const double
     wave_sync();
 }
 
+// 1/sqrt(d) and 1/x to ~1 ulp: hardware estimate + two Newton steps (a few FMAs instead of the
+// ~15-instruction IEEE sqrt / div sequences on the Cholesky critical path)
+__device__ __forceinline__ double rsqrt_nr(double d)
+{
+    double y = __builtin_amdgcn_rsq(d);
+    const double h = 0.5 * d;
+    y = y * fma(-h * y, y, 1.5);
+    y = y * fma(-h * y, y, 1.5);
+    return y;
+}
+__device__ __forceinline__ double rcp_nr(double x)
+{
+    double y = __builtin_amdgcn_rcp(x);
+    double e = fma(-x, y, 1.0);
+    y = fma(y, e, y);
+    e = fma(-x, y, 1.0);
+    return fma(y, e, y);
+}
+
 // ------------------------------------------------------------------------------------------------
 // register Cholesky: lane i (< n) holds row i of the (regularised) KKT matrix in a[0..n-1].
 // Right-looking; column j is broadcast with readlane (uniform lane index, compile-time register).
@@ -672,11 +691,10 @@ __device__ __forceinline__ bool chol_rows(double (&a)[n], double& myidg, int lan
     for (int j = 0; j < n; ++j) {
         const double d = bcast(a[j], j);
         if (!(d > 0.0)) return false;   // wave-uniform
-        const double dj = sqrt(d);
-        const double inv = 1.0 / dj;
+        const double inv = rsqrt_nr(d);
         myidg = lane == j ? inv : myidg;
         const double lij = a[j] * inv;
-        a[j] = lane == j ? dj : lij;
+        a[j] = lane == j ? d * inv : lij;
 #pragma unroll
         for (int k = j + 1; k < n; ++k) a[k] -= lij * bcast(lij, k);
     }
@@ -1153,25 +1171,22 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
             // ---- J layout: gl = J^T y - grad f (OBJ rows carry y = -1)
 #pragma unroll
             for (int T = 0; T < NT; ++T) gl[T] = 0.0;
+            // mo4 == 4 * KSM: every step is a real (possibly padding) row group -> one basic block,
+            // all loads in flight together
 #pragma unroll
             for (int s = 0; s < KSM; ++s) {
-                if (4 * s < mo4) {
-                    const int r = 4 * s + g4;
-                    const uint32_t pk = w.rgen[r];
-                    const double2* rc2 = reinterpret_cast<const double2*>(w.rcoef + 4 * r);
-                    const double2 ca = rc2[0], cb = rc2[1];
-                    const double y = w.ry[r];
+                const int r = 4 * s + g4;
+                const uint32_t pk = w.rgen[r];
+                const double2* rc2 = reinterpret_cast<const double2*>(w.rcoef + 4 * r);
+                const double2 ca = rc2[0], cb = rc2[1];
+                const double y = w.ry[r];
 #pragma unroll
-                    for (int T = 0; T < NT; ++T) {
-                        const int cc = 16 * T + col;
-                        const double j = ca.x * G[gen_i(pk, 0) * NCP + cc] + ca.y * G[gen_i(pk, 1) * NCP + cc] +
-                                         cb.x * G[gen_i(pk, 2) * NCP + cc] + cb.y * G[gen_i(pk, 3) * NCP + cc];
-                        gl[T] += j * y;
-                        if constexpr (JC) jv[JC ? s : 0][T] = j;
-                    }
-                } else if constexpr (JC) {
-#pragma unroll
-                    for (int T = 0; T < NT; ++T) jv[JC ? s : 0][T] = 0.0;
+                for (int T = 0; T < NT; ++T) {
+                    const int cc = 16 * T + col;
+                    const double j = ca.x * G[gen_i(pk, 0) * NCP + cc] + ca.y * G[gen_i(pk, 1) * NCP + cc] +
+                                     cb.x * G[gen_i(pk, 2) * NCP + cc] + cb.y * G[gen_i(pk, 3) * NCP + cc];
+                    gl[T] += j * y;
+                    if constexpr (JC) jv[JC ? s : 0][T] = j;
                 }
             }
 #pragma unroll
@@ -1262,34 +1277,30 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
             for (int T = 0; T < NT; ++T) pw[T] = 0.0;
 #pragma unroll
             for (int s = 0; s < KSM; ++s) {
-                if (4 * s < mo4) {
-                    const int r = 4 * s + g4;
-                    const double sg = w.rsig[r], wr = w.rw[r];
-                    double j[NT];
-                    if constexpr (JC) {
+                const int r = 4 * s + g4;
+                const double sg = w.rsig[r], wr = w.rw[r];   // padding / OBJ rows: sigma = 0
+                double j[NT];
+                if constexpr (JC) {
 #pragma unroll
-                        for (int T = 0; T < NT; ++T) j[T] = jv[JC ? s : 0][T];
-                    } else {
-                        const uint32_t pk = w.rgen[r];
-                        const double2* rc2 = reinterpret_cast<const double2*>(w.rcoef + 4 * r);
-                        const double2 ca = rc2[0], cb = rc2[1];
+                    for (int T = 0; T < NT; ++T) j[T] = jv[JC ? s : 0][T];
+                } else {
+                    const uint32_t pk = w.rgen[r];
+                    const double2* rc2 = reinterpret_cast<const double2*>(w.rcoef + 4 * r);
+                    const double2 ca = rc2[0], cb = rc2[1];
 #pragma unroll
-                        for (int T = 0; T < NT; ++T) {
-                            const int cc = 16 * T + col;
-                            j[T] = ca.x * G[gen_i(pk, 0) * NCP + cc] + ca.y * G[gen_i(pk, 1) * NCP + cc] +
-                                   cb.x * G[gen_i(pk, 2) * NCP + cc] + cb.y * G[gen_i(pk, 3) * NCP + cc];
-                        }
+                    for (int T = 0; T < NT; ++T) {
+                        const int cc = 16 * T + col;
+                        j[T] = ca.x * G[gen_i(pk, 0) * NCP + cc] + ca.y * G[gen_i(pk, 1) * NCP + cc] +
+                               cb.x * G[gen_i(pk, 2) * NCP + cc] + cb.y * G[gen_i(pk, 3) * NCP + cc];
                     }
+                }
 #pragma unroll
-                    for (int T = 0; T < NT; ++T) pw[T] += j[T] * wr;
-                    if (4 * s < mr4) {
-                        d4* a = acc[s & 1];
-                        a[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(j[0], sg * j[0], a[0], 0, 0, 0);
-                        if constexpr (NT == 2) {
-                            a[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(j[0], sg * j[1], a[1], 0, 0, 0);
-                            a[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(j[1], sg * j[1], a[2], 0, 0, 0);
-                        }
-                    }
+                for (int T = 0; T < NT; ++T) pw[T] += j[T] * wr;
+                d4* a = acc[s & 1];
+                a[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(j[0], sg * j[0], a[0], 0, 0, 0);
+                if constexpr (NT == 2) {
+                    a[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(j[0], sg * j[1], a[1], 0, 0, 0);
+                    a[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(j[1], sg * j[1], a[2], 0, 0, 0);
                 }
             }
 #pragma unroll
@@ -1409,10 +1420,11 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
             dZl[q] = HL(q) ? mu * idl[q] - zl[q] - zl[q] * idl[q] * dS[q] : 0.0;
             dZu[q] = HU(q) ? mu * idu[q] - zu[q] + zu[q] * idu[q] * dS[q] : 0.0;
             const double dl = sr[q] - cl[q], du = cu[q] - sr[q];
-            if (HL(q) && dS[q] < 0) ap = fmin(ap, -tau * dl / dS[q]);
-            if (HU(q) && dS[q] > 0) ap = fmin(ap, tau * du / dS[q]);
-            if (HL(q) && dZl[q] < 0) az = fmin(az, -tau * zl[q] / dZl[q]);
-            if (HU(q) && dZu[q] < 0) az = fmin(az, -tau * zu[q] / dZu[q]);
+            const double ids = rcp_nr(dS[q]);
+            if (HL(q) && dS[q] < 0) ap = fmin(ap, -tau * dl * ids);
+            if (HU(q) && dS[q] > 0) ap = fmin(ap, tau * du * ids);
+            if (HL(q) && dZl[q] < 0) az = fmin(az, -tau * zl[q] * rcp_nr(dZl[q]));
+            if (HU(q) && dZu[q] < 0) az = fmin(az, -tau * zu[q] * rcp_nr(dZu[q]));
             theta += fabs(rcv[q]);
             sl += (HL(q) ? dS[q] * idl[q] : 0.0) - (HU(q) ? dS[q] * idu[q] : 0.0);
         }
@@ -1422,12 +1434,13 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
         sl = wsum(sl);
         const double phi = uni(f_cur - mu * lsum_cur);
         const double gphi = uni(gdv - mu * sl);
-        const double pth = uni(pow(theta, sth));
-        const double pgp = uni(gphi < 0 ? pow(-gphi, sph) : 0.0);
+        // switching condition a (-gphi)^s_phi > theta^s_theta in log space: log a + s_phi log(-gphi) >
+        // s_theta log theta (two logs per iteration instead of two pow per trial)
+        const double lsw = uni(gphi < 0 ? sth * log(theta) - sph * log(-gphi) : 0.0);
         double amin;
         if (gphi < 0) {
             amin = fmin(gth, gph * theta / -gphi);
-            if (theta <= w.cst[K_THMIN]) amin = fmin(amin, pth / pgp);
+            if (theta <= w.cst[K_THMIN]) amin = fmin(amin, exp(lsw));
         } else {
             amin = gth;
         }
@@ -1435,6 +1448,7 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
         STAMP(6);
         // ---- filter line search on trial points V + a dV (row registers only)
         double a = ap;
+        double la = uni(log(ap));   // log a, tracked exactly through the halvings
         bool accepted = false, ftype = false;
         double ctr[RPL], ta0[RPL], ta1[RPL], vt[RPL][4];
         double ft = 0.0, lgt = 0.0;
@@ -1472,7 +1486,7 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
                 ok = __ballot(b0 || b1) == 0ull;
             }
             if (ok) {
-                const bool switching = gphi < 0 && a * pgp > pth;
+                const bool switching = gphi < 0 && la > lsw;
                 if (switching && theta <= w.cst[K_THMIN]) {
                     if (pht <= phi + eta * a * gphi) {
                         accepted = true;
@@ -1485,6 +1499,7 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
             }
             if (accepted) break;
             a = uni(a * 0.5);
+            la = uni(la - M_LN2);
         }
         STAMP(7);
         RELANE();
@@ -1571,8 +1586,8 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
             zl[q] += az * dZl[q];
             zu[q] += az * dZu[q];
             const double d1 = sr[q] - cl[q], d2 = cu[q] - sr[q];
-            idl[q] = HL(q) ? 1.0 / d1 : 0.0;
-            idu[q] = HU(q) ? 1.0 / d2 : 0.0;
+            idl[q] = HL(q) ? rcp_nr(d1) : 0.0;
+            idu[q] = HU(q) ? rcp_nr(d2) : 0.0;
             zl[q] = HL(q) ? fmin(fmax(zl[q], mu * 1e-10 * idl[q]), 1e10 * mu * idl[q]) : 0.0;
             zu[q] = HU(q) ? fmin(fmax(zu[q], mu * 1e-10 * idu[q]), 1e10 * mu * idu[q]) : 0.0;
         }
@@ -1887,6 +1902,15 @@ KP make_kp(const Handle* h, long long B, bool solve)
     return P;
 }
 
+// J-layout steps (4 rows each) of the compiled solve kernels; mo4 is rounded up to 4 * ksm_of(rows)
+int ksm_of(int rows)
+{
+    static const int K[] = {8, 10, 12, 16, 24, 32, 48};
+    for (int k : K)
+        if (rows <= 4 * k) return k;
+    return 1 << 20;
+}
+
 template <int N>
 hipError_t launch_t(bool solve, const KP& P, size_t smem, hipStream_t st)
 {
@@ -2048,7 +2072,8 @@ int alipmpc_create(const alipmpc_cfg* cfg, int device, void** handle)
     h->rps_s = h->rps + (cfg->variant == ALIPMPC_VARIANT_MODI ? 1 : 0);   // f_en -> two smooth rows
     h->m_s = cfg->N * h->rps_s;
     h->mr4_s = (h->m_s + 3) & ~3;
-    h->mo4 = h->mr4_s + 4 * ((cfg->N + 3) / 4);   // + the objective pseudo-rows of the solve kernel
+    // + the objective pseudo-rows of the solve kernel, rounded up to the compiled J-layout size (4 KSM)
+    h->mo4 = 4 * ksm_of(h->mr4_s + 4 * ((cfg->N + 3) / 4));
     if (h->mr4 > MAX_ROWS || h->mo4 > MAX_ROWS + 64) {
         delete h;
         return ALIPMPC_EINVAL;
