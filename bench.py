@@ -36,6 +36,15 @@ def flops_per_iter(n, m, N, nobs):
     return kkt + chol + nlp
 
 
+def solve_kernel_name(N, rps, modi):
+    """The solve_kernel<N, KSM> instance the library dispatches (csrc/alipmpc.hip: ksm_of): constraint rows
+    in the solve layout (f_en split into two rows for modi) + N objective rows, in 4-row J-layout steps."""
+    m = N * (rps + (1 if modi else 0))
+    rows = ((m + 3) // 4) * 4 + 4 * ((N + 3) // 4)
+    ksm = next(k for k in (8, 10, 12, 16, 24, 32, 48) if rows <= 4 * k)
+    return f"solve_kernel<{N},{ksm}>", m
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -139,8 +148,8 @@ def main():
     total_solves = world * B * K
     value = total_solves / elapsed
     # roofline of the dominant kernel (solve_kernel): algorithmic FP64 flops per launch / launch time
-    m = N * solver.rps
-    fpi = flops_per_iter(n, N * (4 + args.obstacles + (1 if variant == 0 else 0)), N, args.obstacles)
+    kname, m = solve_kernel_name(N, solver.rps, variant == alipmpc.VARIANT_MODI)
+    fpi = flops_per_iter(n, m, N, args.obstacles)
     launch_flops = fpi * float(iters.sum())
     achieved = launch_flops / (kernel_ms * 1e-3) / 1e12
     traffic = None
@@ -174,14 +183,15 @@ def main():
             "data": "synthetic (rand_obs distribution, SURVEY 8d), generated per rank from (seed, rank)",
             "config": {
                 "workload": f"cfg2: B={B} ALIP initial states per GPU, N={N} horizon, {args.obstacles} circles, "
-                            f"variant={args.variant}, fp64, interior-point to tol 1e-8",
+                            f"variant={args.variant}, fp64, interior point (tol 1e-8, max_iter {cfg.max_iter} = the "
+                            f"reference's IPOPT cap)",
                 "batch_per_gpu": B, "global_batch": B * world, "horizon": N, "obstacles": args.obstacles,
                 "variant": args.variant, "parallelism": f"shard{world}" if world > 1 else "single",
                 "mean_iters": float(iters.mean()), "max_iters": int(iters.max()),
                 "status_counts": {str(k): int(v) for k, v in zip(*np.unique(status, return_counts=True))},
             },
             "roofline": {
-                "kernel": "solve_kernel<3,1>",
+                "kernel": kname,
                 "bound": "mfma",
                 "achieved": achieved,
                 "peak": FP64_PEAK_TFLOPS,

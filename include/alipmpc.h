@@ -95,8 +95,8 @@ typedef struct alipmpc_cfg {
     double mu_init;     /* initial barrier parameter */
 } alipmpc_cfg;
 
-/* Fill *out with the reference's constants for a variant and horizon.  nc_max = ne_max = 6,
- * max_iter = 100, precision fp64. */
+/* Fill *out with the reference's constants for a variant and horizon.  nc_max = ne_max = 6, precision
+ * fp64, max_iter = the reference's IPOPT cap (modi 30, sig_step 20, DD 40). */
 int alipmpc_default_cfg(int32_t variant, int32_t N, alipmpc_cfg* out);
 
 /* Rows per step and total padded rows (m_max) of the fixed constraint layout for cfg. */

@@ -1992,7 +1992,8 @@ int alipmpc_default_cfg(int32_t variant, int32_t N, alipmpc_cfg* c)
     c->nc_max = 6;
     c->ne_max = 6;
     c->variant = variant;
-    c->max_iter = 100;
+    // the reference's IPOPT caps: MPC_LIP_modi.py:287 (30), MPC_LIP_sig_step.py:269 (20), MPC_DD_sig_step.py:183 (40)
+    c->max_iter = variant == ALIPMPC_VARIANT_SIG_STEP ? 20 : variant == ALIPMPC_VARIANT_DD ? 40 : 30;
     c->precision = ALIPMPC_PREC_FP64;
     c->select_obs = 1;
     c->detour = 1;

@@ -86,9 +86,10 @@ def test_setup_matches_reference(gpu_lib, golden, name, variant):
 
 
 def test_solve_sup_learn_recorded_cyipopt(gpu_lib, golden, coracle):
+    # solution parity: run to convergence (max_iter 100 instead of the reference's cap of 30)
     d = golden("g3_sup_learn")
     B = len(d["leg"])
-    cfg = gpu_lib.default_cfg(0, nc_max=6, ne_max=0)
+    cfg = gpu_lib.default_cfg(0, nc_max=6, ne_max=0, max_iter=100)
     s = gpu_lib.Solver(cfg)
     cir = np.tile(d["cir_safe"], (B, 1, 1))
     o = s.solve(d["x_nex"], [10, 10], d["leg"], cir, np.full(B, 6), u0=d["u0"])
@@ -97,7 +98,7 @@ def test_solve_sup_learn_recorded_cyipopt(gpu_lib, golden, coracle):
     assert (err[ok] < 1e-4).sum() >= int(0.97 * ok.sum())
     bt = dict(x0=d["x_nex"], goal=np.tile([10.0, 10.0], (B, 1)), leg=d["leg"], cir=cir, nc=np.full(B, 6),
               u0=d["u0"])
-    ref = _oracle_solve(coracle, dict(variant=0, nc_max=6, ne_max=0), bt)
+    ref = _oracle_solve(coracle, dict(variant=0, nc_max=6, ne_max=0, max_iter=100), bt)
     _compare(o, ref)
 
 
@@ -105,7 +106,7 @@ def test_solve_sup_learn_recorded_cyipopt(gpu_lib, golden, coracle):
 def test_solve_synthetic_scipy_goldens(gpu_lib, golden, variant, name):
     d = golden(f"g3_synthetic_{name}")
     good = (d["agree"] < 1e-8) & (d["viol"] < 1e-8)
-    cfg = gpu_lib.default_cfg(variant, nc_max=6, ne_max=6)
+    cfg = gpu_lib.default_cfg(variant, nc_max=6, ne_max=6, max_iter=100)   # to convergence
     s = gpu_lib.Solver(cfg)
     o = s.solve(d["x0"], d["goal"], d["leg"], d["cir"], d["nc"], d["elp"], d["ne"], u0=d["u0"])
     err = np.max(np.abs(o["foot"] - d["foot_ref"]), axis=1)

@@ -38,6 +38,8 @@ def test_default_cfg_matches_reference_constants():
     assert (s.bvy_hi, s.p, s.q, s.r, s.gamma, s.select_obs) == (0.30, 2.0, 1.0, 15.0, 0.4, 0)
     assert alipmpc.rows_per_step(c) == 4 + 6 + 6 + 1 and alipmpc.rows_per_step(s) == 4 + 6 + 6
     assert alipmpc.num_vars(c) == 15
+    # the reference's IPOPT iteration caps (MPC_LIP_modi.py:287, MPC_LIP_sig_step.py:269)
+    assert (c.max_iter, s.max_iter) == (30, 20)
 
 
 def test_no_device_fails_loudly():

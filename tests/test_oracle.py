@@ -130,7 +130,7 @@ def test_sup_learn_recorded_cyipopt_solutions(golden, coracle):
     the reference solve is infeasible too."""
     d = golden("g3_sup_learn")
     B = len(d["leg"])
-    cfg = coracle.default_cfg(0, nc_max=6, ne_max=0)
+    cfg = coracle.default_cfg(0, nc_max=6, ne_max=0, max_iter=100)   # to convergence (reference cap: 30)
     cir = np.tile(d["cir_safe"], (B, 1, 1))
     r = coracle.solve_batch(cfg, d["x_nex"], [10, 10], d["leg"], cir, np.full(B, 6), None, None, d["u0"], nthreads=8)
     ok = d["ok_ref"].astype(bool)
@@ -145,7 +145,7 @@ def test_synthetic_scipy_solutions(golden, coracle, variant, name):
     d = golden(f"g3_synthetic_{name}")
     good = (d["agree"] < 1e-8) & (d["viol"] < 1e-8)
     B = len(d["leg"])
-    cfg = coracle.default_cfg(variant, nc_max=6, ne_max=6)
+    cfg = coracle.default_cfg(variant, nc_max=6, ne_max=6, max_iter=100)   # to convergence
     r = coracle.solve_batch(cfg, d["x0"], d["goal"], d["leg"], d["cir"], d["nc"], d["elp"], d["ne"], d["u0"])
     err = np.max(np.abs(r["foot"] - d["foot_ref"]), axis=1)
     assert good.sum() >= 20

@@ -12,12 +12,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def pmc(path, kernel):
-    vals = []
+    vals, names = [], set()
     with open(path) as fh:
         for r in csv.DictReader(fh):
             if kernel in r["Kernel_Name"]:
                 vals.append(float(r["Counter_Value"]))
-    return vals
+                names.add(r["Kernel_Name"])
+    return vals, names
 
 
 def main(tag, B=4096, N=3):
@@ -32,12 +33,12 @@ def main(tag, B=4096, N=3):
         p = os.path.join(src, sub)
         if os.path.exists(p):
             shutil.copy(p, os.path.join(dst, name))
-    f = pmc(os.path.join(dst, "pmc_fetch_size.csv"), "solve_kernel")
-    w = pmc(os.path.join(dst, "pmc_write_size.csv"), "solve_kernel")
+    f, names = pmc(os.path.join(dst, "pmc_fetch_size.csv"), "solve_kernel")
+    w, _ = pmc(os.path.join(dst, "pmc_write_size.csv"), "solve_kernel")
     if f and w:
         fetch = sum(f) / len(f) * 1024
         write = sum(w) / len(w) * 1024
-        out = {"B": B, "N": N, "kernel": "solve_kernel<3,1>", "fetch_bytes_per_launch": fetch,
+        out = {"B": B, "N": N, "kernel": sorted(names)[0], "fetch_bytes_per_launch": fetch,
                "write_bytes_per_launch": write, "hbm_bytes_per_launch": fetch + write,
                "source": f"profiles/{tag}/pmc_*_size.csv (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes)"}
         with open(os.path.join(dst, "solve_kernel_traffic.json"), "w") as fh:
