@@ -57,6 +57,9 @@ def parse():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")),
+                    help="threads for the all-cores CPU baseline (the GPU box allots 16)")
+    ap.add_argument("--sweep-batch", type=int, default=65536, help="instances for the Jacobian-sweep roofline")
     return ap.parse_args()
 
 
@@ -163,9 +166,13 @@ def main():
         except Exception:
             traffic = None
 
-    cpu = None
+    sweep = jacobian_sweep(alipmpc, scenes, cfg, args, dev) if (rank == 0 and args.sweep_batch > 0) else None
+
+    cpu = cpu_mt = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(cfg, batch, args.cpu_seconds)
+        # the same C restatement with OpenMP over the host cores this job may use
+        cpu_mt = cpu_baseline(cfg, batch, args.cpu_seconds / 2, threads=args.cpu_threads)
 
     if rank == 0:
         line = {
@@ -203,33 +210,71 @@ def main():
                 "iters_per_launch": int(iters.sum()),
             },
             "cpu_baseline": cpu,
+            "cpu_baseline_allcores": cpu_mt,
+            "jacobian_sweep": sweep,
         }
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()
 
 
-def cpu_baseline(cfg, batch, seconds):
-    """C restatement (oracle/liboracle.so) of the same algorithm, single thread, bounded sample of the
-    same workload; timed on this host."""
+def jacobian_sweep(alipmpc, scenes, cfg, args, dev, reps=10):
+    """HBM roofline of the unfused Jacobian sweep (eval_kernel: f, grad f, c, J of the
+    reference callbacks at given u).  Algorithmic bytes per instance = 8(n + 8 + 3 n_c + 5 n_e) read +
+    8(1 + n + m + m n) written (n = 5N, m = padded rows)."""
+    import torch
+    Bs = args.sweep_batch
+    s = alipmpc.Solver(cfg, device=dev.index)
+    bt = scenes.make_batch(Bs, seed=args.seed * 1000 + 7, n_cir=cfg.nc_max, N=cfg.N, scenes_per_batch=4096)
+    n, m = 5 * cfg.N, cfg.N * s.rps
+    inp = {"x0": torch.from_numpy(bt["x0"]).to(dev), "goal": torch.from_numpy(bt["goal"]).to(dev),
+           "leg": torch.from_numpy(bt["leg"].astype(np.int8)).to(dev), "cir": torch.from_numpy(bt["cir"]).to(dev),
+           "nc": torch.from_numpy(bt["nc"].astype(np.int32)).to(dev), "u": torch.from_numpy(bt["u0"]).to(dev)}
+    out = {"f": torch.empty(Bs, dtype=torch.float64, device=dev),
+           "grad": torch.empty((Bs, n), dtype=torch.float64, device=dev),
+           "c": torch.empty((Bs, m), dtype=torch.float64, device=dev),
+           "J": torch.empty((Bs, m, n), dtype=torch.float64, device=dev)}
+    st = torch.cuda.current_stream(dev)
+    for _ in range(2):
+        s.eval_device(inp, out, stream=st)
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(st)
+        s.eval_device(inp, out, stream=st)
+        b.record(st)
+        torch.cuda.synchronize(dev)
+        ts.append(a.elapsed_time(b))
+    ms = float(np.mean(ts))
+    per = 8 * (n + 8 + 3 * cfg.nc_max) + 8 * (1 + n + m + m * n)
+    gbs = Bs * per / (ms * 1e-3) / 1e9
+    return {"kernel": f"eval_kernel<{cfg.N}>", "bound": "hbm", "batch": Bs, "bytes_per_instance": per,
+            "kernel_ms": ms, "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+            "evals_per_s": Bs / (ms * 1e-3)}
+
+
+def cpu_baseline(cfg, batch, seconds, threads=1):
+    """C restatement (oracle/liboracle.so) of the same algorithm, bounded sample of the same workload,
+    timed on this host (1 thread, or OpenMP over `threads`)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as C
     co = C.default_cfg(cfg.variant, cfg.N, nc_max=cfg.nc_max, ne_max=0)
     B = batch["x0"].shape[0]
     done = 0
     t0 = time.perf_counter()
-    chunk = 64
+    chunk = 64 * threads
     while time.perf_counter() - t0 < seconds:
         i0 = done % B
         i1 = min(i0 + chunk, B)
         C.solve_batch(co, batch["x0"][i0:i1], batch["goal"][i0:i1], batch["leg"][i0:i1], batch["cir"][i0:i1],
                       batch["nc"][i0:i1], np.zeros((i1 - i0, 0, 5)), np.zeros(i1 - i0), batch["u0"][i0:i1],
-                      nthreads=1)
+                      nthreads=threads)
         done += i1 - i0
     dt = time.perf_counter() - t0
-    return {"value": done / dt, "unit": "solves/s", "cores": 1, "kind": "port",
+    return {"value": done / dt, "unit": "solves/s", "cores": threads, "kind": "port",
             "sample": f"{done} instances of the cfg2 workload (first {min(done, B)} of the GPU batch, cycled), "
-                      f"C oracle oracle/alipmpc_oracle.c, same interior-point algorithm, 1 thread, {dt:.1f} s"}
+                      f"C oracle oracle/alipmpc_oracle.c, same interior-point algorithm, {threads} thread(s), "
+                      f"{dt:.1f} s"}
 
 
 if __name__ == "__main__":
