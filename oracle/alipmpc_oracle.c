@@ -46,6 +46,8 @@ typedef struct {
     const oconsts* K;
     int N, n, m, rpk, nc, ne, modi;
     int split;   /* solver-internal: f_en row replaced by the two smooth rows vbx +- s dth <= bvx_hi */
+    int dd;      /* DD (unicycle) instance: x0[0..2] = (px, py, th), decision u = (v, w) x N */
+    double last_u[2];
     double x0[5], goal[2], goal_orig[2];
     double cir[OMAXO][3], elp[OMAXO][5];
     double eqa[OMAXO], eqb[OMAXO], eqc[OMAXO], ek[OMAXO];
@@ -622,6 +624,278 @@ static double barrier(double f, const double* s, const double* cl, const double*
     return f - mu * acc;
 }
 
+/* ------------------------------------------------------------------------------------------------ */
+/* DD variant (MPC_DD_sig_step.py): x_{i+1} = x_i + [T v_i cos th_i, T v_i sin th_i, w_i] (:355-360)   */
+/* rows per step: reference [cbf circles, cbf ellipses, f_en = s|w| + v] (:131-141, :410-420); solver  */
+/* (split): [cbf..., v + s w <= v_max, v - s w <= v_max, v in [v_min, v_max], w in [-w_max, w_max]]    */
+/* ------------------------------------------------------------------------------------------------ */
+static void oprob_init_dd(oprob* P, const alipmpc_cfg* cfg, const double* x0, const double* goal, const double* cir,
+                          int nc, const double* elp, int ne, const double* last_u, int split)
+{
+    memset(P, 0, sizeof(*P));
+    P->cfg = cfg;
+    P->N = cfg->N;
+    P->n = 2 * cfg->N;
+    P->dd = 1;
+    P->split = split;
+    memcpy(P->x0, x0, 3 * sizeof(double));
+    P->goal[0] = P->goal_orig[0] = goal[0];
+    P->goal[1] = P->goal_orig[1] = goal[1];
+    P->last_u[0] = last_u ? last_u[0] : 0.0;
+    P->last_u[1] = last_u ? last_u[1] : 0.0;
+    for (int j = 0; j < nc; ++j) {       /* all obstacles: select_obs is commented out (:75) */
+        memcpy(P->cir[P->nc], cir + 3 * j, 3 * sizeof(double));
+        P->sel_c[P->nc++] = j;
+    }
+    for (int j = 0; j < ne; ++j) {
+        memcpy(P->elp[P->ne], elp + 5 * j, 5 * sizeof(double));
+        P->sel_e[P->ne++] = j;
+    }
+    for (int j = 0; j < P->ne; ++j) {
+        const double* e = P->elp[j];
+        double ce = cos(e[4]), se = sin(e[4]);
+        P->eqa[j] = (e[3] * ce) * (e[3] * ce) + (e[2] * se) * (e[2] * se);
+        P->eqb[j] = 2 * ce * se * (e[3] * e[3] - e[2] * e[2]);
+        P->eqc[j] = (e[3] * se) * (e[3] * se) + (e[2] * ce) * (e[2] * ce);
+        P->ek[j] = (e[3] * e[2]) * (e[3] * e[2]);
+    }
+    const int nob = P->nc + P->ne;
+    P->rpk = nob + (split ? 4 : 1);
+    P->m = P->N * P->rpk;
+    int r = 0;
+    for (int k = 0; k < P->N; ++k) {
+        for (int j = 0; j < nob; ++j) {
+            P->cl[r] = 0.0;
+            P->cu[r++] = INFINITY;
+        }
+        if (split) {
+            P->cl[r] = -INFINITY; P->cu[r++] = cfg->bvx_hi;
+            P->cl[r] = -INFINITY; P->cu[r++] = cfg->bvx_hi;
+            P->cl[r] = cfg->bvx_lo; P->cu[r++] = cfg->bvx_hi;
+            P->cl[r] = -cfg->dtheta_max; P->cu[r++] = cfg->dtheta_max;
+        } else {
+            P->cl[r] = cfg->bvx_lo;
+            P->cu[r++] = cfg->bvx_hi;
+        }
+    }
+}
+
+static void dd_rollout(const oprob* P, const double* u, double X[][3])
+{
+    const double T = P->cfg->dt;
+    X[0][0] = P->x0[0]; X[0][1] = P->x0[1]; X[0][2] = P->x0[2];
+    for (int i = 0; i < P->N; ++i) {
+        const double v = u[2 * i], w = u[2 * i + 1], th = X[i][2];
+        X[i + 1][0] = X[i][0] + T * v * cos(th);
+        X[i + 1][1] = X[i][1] + T * v * sin(th);
+        X[i + 1][2] = X[i][2] + w;
+    }
+}
+
+/* Jp[k][c][a] = d x_k[c] / d u_a (closed forms of cal_dx_du, :534-566) */
+static void dd_dpos(const oprob* P, double X[][3], double Jp[][3][2 * OMAXN])
+{
+    const double T = P->cfg->dt;
+    const int n = P->n;
+    memset(Jp, 0, sizeof(double) * (P->N + 1) * 3 * 2 * OMAXN);
+    for (int k = 1; k <= P->N; ++k)
+        for (int j = 0; j < k; ++j) {
+            Jp[k][0][2 * j] = T * cos(X[j][2]);
+            Jp[k][1][2 * j] = T * sin(X[j][2]);
+            Jp[k][0][2 * j + 1] = -(X[k][1] - X[j + 1][1]);
+            Jp[k][1][2 * j + 1] = X[k][0] - X[j + 1][0];
+            Jp[k][2][2 * j + 1] = 1.0;
+        }
+    (void)n;
+}
+
+static double dd_objective(const oprob* P, const double* u)
+{
+    const alipmpc_cfg* c = P->cfg;
+    double X[OMAXN + 1][3];
+    dd_rollout(P, u, X);
+    double f = 0, up0 = P->last_u[0], up1 = P->last_u[1];
+    for (int i = 0; i < P->N; ++i) {
+        double dx = X[i + 1][0] - P->goal[0], dy = X[i + 1][1] - P->goal[1];
+        double tar = atan2(P->goal[1] - X[i + 1][1], P->goal[0] - X[i + 1][0]);
+        double d0 = u[2 * i] - up0, d1 = u[2 * i + 1] - up1;
+        f += c->q * (dx * dx + dy * dy) + c->r * (X[i + 1][2] - tar) * (X[i + 1][2] - tar) + c->dd_t * (d0 * d0 + d1 * d1);
+        up0 = u[2 * i];
+        up1 = u[2 * i + 1];
+    }
+    double dx = X[1][0] - P->goal[0], dy = X[1][1] - P->goal[1];
+    return f + c->p * (dx * dx + dy * dy);
+}
+
+static void dd_gradient(const oprob* P, const double* u, double* g)
+{
+    const alipmpc_cfg* c = P->cfg;
+    double X[OMAXN + 1][3], Jp[OMAXN + 1][3][2 * OMAXN];
+    dd_rollout(P, u, X);
+    dd_dpos(P, X, Jp);
+    const int n = P->n;
+    for (int a = 0; a < n; ++a) g[a] = 0;
+    for (int k = 1; k <= P->N; ++k) {
+        double w = c->q + (k == 1 ? c->p : 0.0);
+        double dxg = P->goal[0] - X[k][0], dyg = P->goal[1] - X[k][1];
+        double rho2 = dxg * dxg + dyg * dyg, phi = X[k][2] - atan2(dyg, dxg);
+        for (int a = 0; a < n; ++a)
+            g[a] += 2 * w * (-dxg * Jp[k][0][a] - dyg * Jp[k][1][a]) +
+                    2 * c->r * phi * (Jp[k][2][a] - (dyg * Jp[k][0][a] - dxg * Jp[k][1][a]) / rho2);
+    }
+    double up0 = P->last_u[0], up1 = P->last_u[1];
+    for (int i = 0; i < P->N; ++i) {
+        double d0 = u[2 * i] - up0, d1 = u[2 * i + 1] - up1;
+        g[2 * i] += 2 * c->dd_t * d0;
+        g[2 * i + 1] += 2 * c->dd_t * d1;
+        if (i > 0) {
+            g[2 * i - 2] -= 2 * c->dd_t * d0;
+            g[2 * i - 1] -= 2 * c->dd_t * d1;
+        }
+        up0 = u[2 * i];
+        up1 = u[2 * i + 1];
+    }
+}
+
+static void dd_constraints(const oprob* P, const double* u, double* out)
+{
+    const alipmpc_cfg* c = P->cfg;
+    double X[OMAXN + 1][3];
+    dd_rollout(P, u, X);
+    double gm1 = c->gamma - 1.0;
+    int r = 0;
+    for (int i = 0; i < P->N; ++i) {
+        for (int j = 0; j < P->nc + P->ne; ++j) out[r++] = h_obs(P, j, X[i + 1][0], X[i + 1][1]) + gm1 * h_obs(P, j, X[i][0], X[i][1]);
+        const double v = u[2 * i], w = u[2 * i + 1];
+        if (P->split) {
+            out[r++] = v + c->s * w;
+            out[r++] = v - c->s * w;
+            out[r++] = v;
+            out[r++] = w;
+        } else {
+            out[r++] = c->s * fabs(w) + v;
+        }
+    }
+}
+
+static void dd_jacobian(const oprob* P, const double* u, double* J)
+{
+    const alipmpc_cfg* c = P->cfg;
+    double X[OMAXN + 1][3], Jp[OMAXN + 1][3][2 * OMAXN];
+    dd_rollout(P, u, X);
+    dd_dpos(P, X, Jp);
+    const int n = P->n;
+    double gm1 = c->gamma - 1.0;
+    int r = 0;
+    for (int i = 0; i < P->N; ++i) {
+        for (int o = 0; o < P->nc + P->ne; ++o) {
+            double g0, g1, h0, h1;
+            dh_obs(P, o, X[i + 1][0], X[i + 1][1], &g0, &g1);
+            dh_obs(P, o, X[i][0], X[i][1], &h0, &h1);
+            for (int a = 0; a < n; ++a)
+                J[(size_t)r * n + a] = g0 * Jp[i + 1][0][a] + g1 * Jp[i + 1][1][a] + gm1 * (h0 * Jp[i][0][a] + h1 * Jp[i][1][a]);
+            r++;
+        }
+        const double w = u[2 * i + 1];
+        const int nrow = P->split ? 4 : 1;
+        for (int t = 0; t < nrow; ++t)
+            for (int a = 0; a < n; ++a) J[(size_t)(r + t) * n + a] = 0.0;
+        if (P->split) {
+            J[(size_t)r * n + 2 * i] = 1.0; J[(size_t)r * n + 2 * i + 1] = c->s; r++;
+            J[(size_t)r * n + 2 * i] = 1.0; J[(size_t)r * n + 2 * i + 1] = -c->s; r++;
+            J[(size_t)r * n + 2 * i] = 1.0; r++;
+            J[(size_t)r * n + 2 * i + 1] = 1.0; r++;
+        } else {
+            J[(size_t)r * n + 2 * i] = 1.0;
+            J[(size_t)r * n + 2 * i + 1] = c->s * (w == 0 ? 0.0 : copysign(1.0, w));   /* den_du :505-510 */
+            r++;
+        }
+    }
+}
+
+/* exact Hessian of L = f - y^T c, including the second derivatives of the unicycle rollout */
+static void dd_hessian(const oprob* P, const double* u, const double* y, double* H)
+{
+    const alipmpc_cfg* c = P->cfg;
+    const double T = c->dt;
+    double X[OMAXN + 1][3], Jp[OMAXN + 1][3][2 * OMAXN];
+    dd_rollout(P, u, X);
+    dd_dpos(P, X, Jp);
+    const int n = P->n, N = P->N, nob = P->nc + P->ne;
+    const double gm1 = c->gamma - 1.0;
+    double Hl[OMAXN + 1][3][3], gl[OMAXN + 1][2];
+    memset(Hl, 0, sizeof(Hl));
+    memset(gl, 0, sizeof(gl));
+    for (int k = 1; k <= N; ++k) {
+        double w = c->q + (k == 1 ? c->p : 0.0);
+        double dxg = P->goal[0] - X[k][0], dyg = P->goal[1] - X[k][1];
+        double rho2 = dxg * dxg + dyg * dyg, phi = X[k][2] - atan2(dyg, dxg), r4 = rho2 * rho2;
+        double gp[3] = {-dyg / rho2, dxg / rho2, 1.0};
+        for (int a = 0; a < 3; ++a)
+            for (int b = 0; b < 3; ++b) Hl[k][a][b] += 2 * c->r * gp[a] * gp[b];
+        Hl[k][0][0] += 2 * w;
+        Hl[k][1][1] += 2 * w;
+        double s00 = 2 * dxg * dyg / r4, s01 = (dyg * dyg - dxg * dxg) / r4, s11 = -2 * dxg * dyg / r4;
+        Hl[k][0][0] -= 2 * c->r * phi * s00;
+        Hl[k][0][1] -= 2 * c->r * phi * s01;
+        Hl[k][1][0] -= 2 * c->r * phi * s01;
+        Hl[k][1][1] -= 2 * c->r * phi * s11;
+        gl[k][0] = -2 * w * dxg + 2 * c->r * phi * gp[0];
+        gl[k][1] = -2 * w * dyg + 2 * c->r * phi * gp[1];
+    }
+    for (int i = 0; i < N; ++i) {
+        const double* yk = y + i * P->rpk;
+        for (int o = 0; o < nob; ++o) {
+            double q00, q01, q11;
+            if (o < P->nc) {
+                q00 = 2; q01 = 0; q11 = 2;
+            } else {
+                int e = o - P->nc;
+                q00 = 2 * P->eqa[e]; q01 = P->eqb[e]; q11 = 2 * P->eqc[e];
+            }
+            double g0, g1, h0, h1;
+            dh_obs(P, o, X[i + 1][0], X[i + 1][1], &g0, &g1);
+            dh_obs(P, o, X[i][0], X[i][1], &h0, &h1);
+            Hl[i + 1][0][0] -= yk[o] * q00; Hl[i + 1][0][1] -= yk[o] * q01;
+            Hl[i + 1][1][0] -= yk[o] * q01; Hl[i + 1][1][1] -= yk[o] * q11;
+            gl[i + 1][0] -= yk[o] * g0; gl[i + 1][1] -= yk[o] * g1;
+            if (i >= 1) {
+                Hl[i][0][0] -= yk[o] * gm1 * q00; Hl[i][0][1] -= yk[o] * gm1 * q01;
+                Hl[i][1][0] -= yk[o] * gm1 * q01; Hl[i][1][1] -= yk[o] * gm1 * q11;
+                gl[i][0] -= yk[o] * gm1 * h0; gl[i][1] -= yk[o] * gm1 * h1;
+            }
+        }
+    }
+    for (int a = 0; a < n * n; ++a) H[a] = 0;
+    for (int k = 1; k <= N; ++k)
+        for (int a = 0; a < n; ++a)
+            for (int b = 0; b < n; ++b) {
+                double acc = 0;
+                for (int p = 0; p < 3; ++p)
+                    for (int q = 0; q < 3; ++q) acc += Jp[k][p][a] * Hl[k][p][q] * Jp[k][q][b];
+                const int ja = a / 2, jb = b / 2, va = (a % 2) == 0, vb = (b % 2) == 0;
+                double sxx = 0, syy = 0;
+                if (va && !vb) {
+                    if (jb < ja && ja < k) { sxx = -T * sin(X[ja][2]); syy = T * cos(X[ja][2]); }
+                } else if (vb && !va) {
+                    if (ja < jb && jb < k) { sxx = -T * sin(X[jb][2]); syy = T * cos(X[jb][2]); }
+                } else if (!va && !vb) {
+                    int mm = ja > jb ? ja : jb;
+                    if (mm < k) { sxx = -(X[k][0] - X[mm + 1][0]); syy = -(X[k][1] - X[mm + 1][1]); }
+                }
+                H[a * n + b] += acc + gl[k][0] * sxx + gl[k][1] * syy;
+            }
+    for (int i = 0; i < N; ++i)
+        for (int cc = 0; cc < 2; ++cc) {
+            int a = 2 * i + cc;
+            H[a * n + a] += 2 * c->dd_t * (i < N - 1 ? 2.0 : 1.0);
+            if (i < N - 1) {
+                H[a * n + a + 2] -= 2 * c->dd_t;
+                H[(a + 2) * n + a] -= 2 * c->dd_t;
+            }
+        }
+}
+
 typedef struct {
     int iters, status, restorations;
 } osolve_info;
@@ -641,18 +915,27 @@ static void u_of_p(const oprob* P, const double* pv, double* u)
 }
 static double pobj(const oprob* P, const double* pv)
 {
+    if (P->dd) return dd_objective(P, pv);
     double u[OMAXV];
     u_of_p(P, pv, u);
     return oracle_objective(P, u);
 }
 static void pcons(const oprob* P, const double* pv, double* c)
 {
+    if (P->dd) {
+        dd_constraints(P, pv, c);
+        return;
+    }
     double u[OMAXV];
     u_of_p(P, pv, u);
     constraints(P, u, c);
 }
 static void pgrad(const oprob* P, const double* pv, double* gp)
 {
+    if (P->dd) {
+        dd_gradient(P, pv, gp);
+        return;
+    }
     double u[OMAXV], gu[OMAXV];
     u_of_p(P, pv, u);
     gradient(P, u, gu);
@@ -666,6 +949,10 @@ static void pgrad(const oprob* P, const double* pv, double* gp)
 static void pjac(const oprob* P, const double* pv, double* Jp)
 {
     static __thread double Ju[OMAXM * OMAXV];
+    if (P->dd) {
+        dd_jacobian(P, pv, Jp);
+        return;
+    }
     double u[OMAXV];
     u_of_p(P, pv, u);
     jacobian(P, u, Ju);
@@ -679,6 +966,10 @@ static void pjac(const oprob* P, const double* pv, double* Jp)
 }
 static void phess(const oprob* P, const double* pv, const double* y, double* Hp)
 {
+    if (P->dd) {
+        dd_hessian(P, pv, y, Hp);
+        return;
+    }
     double u[OMAXV], Hu[OMAXV * OMAXV], T[OMAXV * 3 * OMAXN];
     u_of_p(P, pv, u);
     hessian(P, u, y, Hu);
@@ -705,8 +996,8 @@ static void phess(const oprob* P, const double* pv, const double* y, double* Hp)
 static void osolve(oprob* P, const double* u0, double* uout, osolve_info* info)
 {
     const alipmpc_cfg* cfg = P->cfg;
-    const int n = 3 * P->N, m = P->m;
-    double u[OMAXV];   /* the decision: footholds p (n = 3N) */
+    const int n = P->dd ? 2 * P->N : 3 * P->N, m = P->m;
+    double u[OMAXV];   /* the decision: footholds p (n = 3N), DD controls (n = 2N) */
     double cl[OMAXM], cu[OMAXM];
     int hl[OMAXM], hu[OMAXM];
     int nb = 0;
@@ -717,7 +1008,9 @@ static void osolve(oprob* P, const double* u0, double* uout, osolve_info* info)
         cl[i] = hl[i] ? P->cl[i] - 1e-8 * fmax(1.0, fabs(P->cl[i])) : -INFINITY;
         cu[i] = hu[i] ? P->cu[i] + 1e-8 * fmax(1.0, fabs(P->cu[i])) : INFINITY;
     }
-    {
+    if (P->dd) {
+        memcpy(u, u0, sizeof(double) * n);
+    } else {
         double X0[OMAXN + 1][5], Pp0[OMAXN][3];
         rollout(P, u0, X0, Pp0);
         for (int k = 0; k < P->N; ++k)
@@ -939,7 +1232,10 @@ static void osolve(oprob* P, const double* u0, double* uout, osolve_info* info)
         else if (viol > 1e-4)
             status = 2;
     }
-    u_of_p(P, u, uout);
+    if (P->dd)
+        memcpy(uout, u, sizeof(double) * n);
+    else
+        u_of_p(P, u, uout);
     info->iters = it;
     info->status = status;
     info->restorations = n_rest;
@@ -949,6 +1245,7 @@ static void osolve(oprob* P, const double* u0, double* uout, osolve_info* info)
 /* batch entry points (same argument meaning as alipmpc_solve_batch / alipmpc_eval_batch, host memory) */
 int oracle_rows_per_step(const alipmpc_cfg* cfg)
 {
+    if (cfg->variant == ALIPMPC_VARIANT_DD) return cfg->nc_max + cfg->ne_max + 1;
     return 4 + cfg->nc_max + cfg->ne_max + (cfg->variant == ALIPMPC_VARIANT_MODI);
 }
 
@@ -1042,5 +1339,92 @@ int oracle_eval_batch(const alipmpc_cfg* cfg, int64_t B, const double* x0, const
     free(Jc);
     free(P);
     free(K);
+    return 0;
+}
+
+/* DD batch entry points: x0 B x 3, u0/u B x 2N, last_u B x 2; foot_out = first control [v, w, 0];
+ * x_pred = x_1..x_N (B x N x 3) */
+int oracle_solve_batch_dd(const alipmpc_cfg* cfg, int64_t B, const double* x0, const double* goal, const double* cir,
+                          const int32_t* nc, const double* elp, const int32_t* ne, const double* u0,
+                          const double* last_u, double* u_out, double* foot_out, double* x_pred, int32_t* status,
+                          int32_t* iters, int32_t* restorations, int nthreads)
+{
+    if (cfg->variant != ALIPMPC_VARIANT_DD || cfg->N < 1 || cfg->N > OMAXN) return ALIPMPC_EUNSUPPORTED;
+    const int n = 2 * cfg->N;
+#pragma omp parallel for schedule(dynamic, 4) num_threads(nthreads > 0 ? nthreads : 1)
+    for (int64_t b = 0; b < B; ++b) {
+        oprob* P = (oprob*)malloc(sizeof(oprob));
+        oprob_init_dd(P, cfg, x0 + 3 * b, goal + 2 * b, cir + (size_t)3 * cfg->nc_max * b, nc[b],
+                      elp ? elp + (size_t)5 * cfg->ne_max * b : NULL, ne ? ne[b] : 0, last_u ? last_u + 2 * b : NULL,
+                      1);
+        double u[OMAXV];
+        osolve_info info;
+        osolve(P, u0 + (size_t)n * b, u, &info);
+        if (u_out) memcpy(u_out + (size_t)n * b, u, sizeof(double) * n);
+        double X[OMAXN + 1][3];
+        dd_rollout(P, u, X);
+        if (foot_out) {
+            foot_out[3 * b] = u[0];
+            foot_out[3 * b + 1] = u[1];
+            foot_out[3 * b + 2] = 0.0;
+        }
+        if (x_pred)
+            for (int k = 0; k < cfg->N; ++k) memcpy(x_pred + ((size_t)b * cfg->N + k) * 3, X[k + 1], 3 * sizeof(double));
+        if (status) status[b] = info.status;
+        if (iters) iters[b] = info.iters;
+        if (restorations) restorations[b] = info.restorations;
+        free(P);
+    }
+    return 0;
+}
+
+/* reference DD callbacks in the padded layout [circle slots nc_max, ellipse slots ne_max, f_en] per step */
+int oracle_eval_batch_dd(const alipmpc_cfg* cfg, int64_t B, const double* x0, const double* goal, const double* cir,
+                         const int32_t* nc, const double* elp, const int32_t* ne, const double* u,
+                         const double* last_u, double* f, double* grad, double* c, double* J, double* cl, double* cu,
+                         int8_t* row_active)
+{
+    if (cfg->variant != ALIPMPC_VARIANT_DD || cfg->N < 1 || cfg->N > OMAXN) return ALIPMPC_EUNSUPPORTED;
+    const int n = 2 * cfg->N;
+    const int rps = cfg->nc_max + cfg->ne_max + 1, mmax = cfg->N * rps;
+    oprob* P = (oprob*)malloc(sizeof(oprob));
+    double* Jc = (double*)malloc(sizeof(double) * OMAXM * OMAXV);
+    double cc[OMAXM];
+    for (int64_t b = 0; b < B; ++b) {
+        oprob_init_dd(P, cfg, x0 + 3 * b, goal + 2 * b, cir + (size_t)3 * cfg->nc_max * b, nc[b],
+                      elp ? elp + (size_t)5 * cfg->ne_max * b : NULL, ne ? ne[b] : 0, last_u ? last_u + 2 * b : NULL,
+                      0);
+        const double* ub = u + (size_t)n * b;
+        if (f) f[b] = dd_objective(P, ub);
+        if (grad) dd_gradient(P, ub, grad + (size_t)n * b);
+        dd_constraints(P, ub, cc);
+        dd_jacobian(P, ub, Jc);
+        for (int k = 0; k < cfg->N; ++k) {
+            int src = k * P->rpk, dst = k * rps;
+            int map[1 + 2 * OMAXO];
+            int q = 0;
+            for (int j = 0; j < P->nc; ++j) map[q++] = dst + j;
+            for (int j = 0; j < P->ne; ++j) map[q++] = dst + cfg->nc_max + j;
+            map[q++] = dst + cfg->nc_max + cfg->ne_max;
+            for (int r = dst; r < dst + rps; ++r) {
+                if (c) c[(size_t)b * mmax + r] = 0;
+                if (J)
+                    for (int j = 0; j < n; ++j) J[((size_t)b * mmax + r) * n + j] = 0;
+                if (cl) cl[(size_t)b * mmax + r] = -INFINITY;
+                if (cu) cu[(size_t)b * mmax + r] = INFINITY;
+                if (row_active) row_active[(size_t)b * mmax + r] = 0;
+            }
+            for (int t = 0; t < q; ++t) {
+                int r = map[t];
+                if (c) c[(size_t)b * mmax + r] = cc[src + t];
+                if (J) memcpy(J + ((size_t)b * mmax + r) * n, Jc + (size_t)(src + t) * n, sizeof(double) * n);
+                if (cl) cl[(size_t)b * mmax + r] = P->cl[src + t];
+                if (cu) cu[(size_t)b * mmax + r] = P->cu[src + t];
+                if (row_active) row_active[(size_t)b * mmax + r] = 1;
+            }
+        }
+    }
+    free(Jc);
+    free(P);
     return 0;
 }

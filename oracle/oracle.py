@@ -45,6 +45,10 @@ def lib():
         L.oracle_solve_batch.restype = ctypes.c_int
         L.oracle_eval_batch.argtypes = [ctypes.POINTER(Cfg), ctypes.c_int64] + [P] * 16
         L.oracle_eval_batch.restype = ctypes.c_int
+        L.oracle_solve_batch_dd.argtypes = [ctypes.POINTER(Cfg), ctypes.c_int64] + [P] * 14 + [ctypes.c_int]
+        L.oracle_solve_batch_dd.restype = ctypes.c_int
+        L.oracle_eval_batch_dd.argtypes = [ctypes.POINTER(Cfg), ctypes.c_int64] + [P] * 15
+        L.oracle_eval_batch_dd.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -58,10 +62,12 @@ def default_cfg(variant=VARIANT_MODI, N=3, **kw):
 
 
 def n_vars(cfg):
-    return 5 * cfg.N
+    return 2 * cfg.N if cfg.variant == VARIANT_DD else 5 * cfg.N
 
 
 def rows_per_step(cfg):
+    if cfg.variant == VARIANT_DD:
+        return cfg.nc_max + cfg.ne_max + 1
     return 4 + cfg.nc_max + cfg.ne_max + (1 if cfg.variant == VARIANT_MODI else 0)
 
 
@@ -112,4 +118,50 @@ def eval_batch(cfg, x0, goal, leg, cir, nc, elp, ne, u):
                                  _p(out["cu"]), _p(out["goal_eff"]), _p(out["row_active"]))
     if rc != 0:
         raise RuntimeError(f"oracle_eval_batch failed: {rc}")
+    return out
+
+
+def _dd_inputs(cfg, x0, goal, cir, nc, elp, ne, last_u):
+    B = len(x0)
+    x0 = np.ascontiguousarray(x0, np.float64).reshape(B, 3)
+    goal = np.ascontiguousarray(np.broadcast_to(np.asarray(goal, np.float64), (B, 2)))
+    cir = np.ascontiguousarray(cir, np.float64).reshape(B, cfg.nc_max, 3)
+    nc = np.ascontiguousarray(nc, np.int32).reshape(B)
+    if cfg.ne_max > 0 and elp is not None:
+        elp = np.ascontiguousarray(elp, np.float64).reshape(B, cfg.ne_max, 5)
+        ne = np.ascontiguousarray(ne, np.int32).reshape(B)
+    else:
+        elp = None
+        ne = np.zeros(B, np.int32)
+    last_u = np.ascontiguousarray(np.broadcast_to(np.asarray(last_u, np.float64), (B, 2)))
+    return B, x0, goal, cir, nc, elp, ne, last_u
+
+
+def solve_batch_dd(cfg, x0, goal, cir, nc, elp, ne, u0, last_u, nthreads=1):
+    """DD (unicycle) solves; foot = first control [v, w, 0], x_pred = x_1..x_N (B x N x 3)."""
+    B, x0, goal, cir, nc, elp, ne, last_u = _dd_inputs(cfg, x0, goal, cir, nc, elp, ne, last_u)
+    n = n_vars(cfg)
+    u0 = np.ascontiguousarray(u0, np.float64).reshape(B, n)
+    out = dict(u=np.zeros((B, n)), foot=np.zeros((B, 3)), x_pred=np.zeros((B, cfg.N, 3)),
+               status=np.zeros(B, np.int32), iters=np.zeros(B, np.int32), restorations=np.zeros(B, np.int32))
+    rc = lib().oracle_solve_batch_dd(ctypes.byref(cfg), B, _p(x0), _p(goal), _p(cir), _p(nc), _p(elp), _p(ne),
+                                     _p(u0), _p(last_u), _p(out["u"]), _p(out["foot"]), _p(out["x_pred"]),
+                                     _p(out["status"]), _p(out["iters"]), _p(out["restorations"]), nthreads)
+    if rc != 0:
+        raise RuntimeError(f"oracle_solve_batch_dd failed: {rc}")
+    return out
+
+
+def eval_batch_dd(cfg, x0, goal, cir, nc, elp, ne, u, last_u):
+    B, x0, goal, cir, nc, elp, ne, last_u = _dd_inputs(cfg, x0, goal, cir, nc, elp, ne, last_u)
+    n = n_vars(cfg)
+    mm = cfg.N * rows_per_step(cfg)
+    u = np.ascontiguousarray(u, np.float64).reshape(B, n)
+    out = dict(f=np.zeros(B), grad=np.zeros((B, n)), c=np.zeros((B, mm)), J=np.zeros((B, mm, n)),
+               cl=np.zeros((B, mm)), cu=np.zeros((B, mm)), row_active=np.zeros((B, mm), np.int8))
+    rc = lib().oracle_eval_batch_dd(ctypes.byref(cfg), B, _p(x0), _p(goal), _p(cir), _p(nc), _p(elp), _p(ne), _p(u),
+                                    _p(last_u), _p(out["f"]), _p(out["grad"]), _p(out["c"]), _p(out["J"]),
+                                    _p(out["cl"]), _p(out["cu"]), _p(out["row_active"]))
+    if rc != 0:
+        raise RuntimeError(f"oracle_eval_batch_dd failed: {rc}")
     return out

@@ -167,3 +167,60 @@ def test_numpy_and_c_oracles_agree(golden, coracle):
         if st == r["status"][j] and (st != 0 or np.max(np.abs(u - r["u"][j])) < 1e-6):
             agree += 1
     assert agree >= int(0.9 * len(idx))
+
+
+# ---------------------------------------------------------------- DD variant (MPC_DD_sig_step.py)
+def test_dd_callbacks_match_reference(golden, coracle):
+    """numpy + C restatements of the DD LIP_Prob callbacks (MPC_DD_sig_step.py:351-477) vs the goldens."""
+    g = golden("g1_callbacks_dd")
+    cfg = O.default_cfg(2)
+    for t in range(len(g["f"])):
+        nc, ne, m = g["nc"][t], g["ne"][t], g["m"][t]
+        pr = O.DDProblem(cfg, g["x0"][t], g["goal"][t], g["cir"][t][:nc], g["elp"][t][:ne], g["last_u"][t])
+        u = g["u"][t]
+        assert rel(pr.objective(u), g["f"][t]) < REL
+        assert rel(pr.gradient(u), g["grad"][t]) < REL
+        assert rel(pr.constraints(u), g["c"][t][:m]) < REL
+        assert rel(pr.jacobian(u), g["J"][t][:m]) < REL
+    cc = coracle.default_cfg(2, nc_max=6, ne_max=6)
+    r = coracle.eval_batch_dd(cc, g["x0"], g["goal"], g["cir"], g["nc"], g["elp"], g["ne"], g["u"], g["last_u"])
+    assert rel(r["f"], g["f"]) < REL and rel(r["grad"], g["grad"]) < REL
+    for t in range(len(g["f"])):
+        act = r["row_active"][t].astype(bool)
+        assert rel(r["c"][t][act], g["c"][t][:g["m"][t]]) < REL
+        assert rel(r["J"][t][act], g["J"][t][:g["m"][t]]) < REL
+
+
+def test_dd_hessian_matches_finite_differences(golden):
+    g = golden("g1_callbacks_dd")
+    cfg = O.default_cfg(2)
+    rng = np.random.default_rng(5)
+    for t in range(8):
+        nc, ne = g["nc"][t], g["ne"][t]
+        pr = O.DDProblem(cfg, g["x0"][t], g["goal"][t], g["cir"][t][:nc], g["elp"][t][:ne], g["last_u"][t],
+                         split=True)
+        u, y = g["u"][t], rng.normal(0, 1, pr.m)
+        H = pr.hessian(u, y)
+        L = lambda v: pr.gradient(v) - pr.jacobian(v).T @ y
+        Hf = np.stack([(L(u + e) - L(u - e)) / 2e-6 for e in np.eye(pr.n) * 1e-6], 1)
+        assert np.max(np.abs(H - Hf)) / (1 + np.max(np.abs(Hf))) < 1e-7
+
+
+def test_dd_solutions_match_scipy_goldens(golden, coracle):
+    """DD scenes solved by SLSQP and trust-constr on the reference callbacks (tools/gen_goldens.py g3dd)."""
+    d = golden("g3_synthetic_dd")
+    good = (d["agree"] < 1e-6) & (d["viol"] < 1e-8)
+    assert good.sum() >= 20
+    cfg = coracle.default_cfg(2, nc_max=6, ne_max=6, max_iter=100)   # to convergence (reference cap: 40)
+    r = coracle.solve_batch_dd(cfg, d["x0"], d["goal"], d["cir"], d["nc"], d["elp"], d["ne"], d["u0"], d["last_u"])
+    err = np.max(np.abs(r["u"] - d["u_ref"]), axis=1)
+    assert np.all(err[good] < 1e-4), err[good].max()
+    # numpy restatement agrees with the C one
+    pcfg = O.default_cfg(2)
+    for t in range(0, len(d["u0"]), 4):
+        pr = O.DDProblem(pcfg, d["x0"][t], d["goal"][t], d["cir"][t][:d["nc"][t]], d["elp"][t][:d["ne"][t]],
+                         d["last_u"][t])
+        u, st, it = O.dd_solve(pr, d["u0"][t], max_iter=100)
+        assert st == r["status"][t]
+        if st == 0:
+            assert np.max(np.abs(u - r["u"][t])) < 1e-6

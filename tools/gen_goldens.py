@@ -17,7 +17,7 @@ Fixtures written
   g3_sup_learn.npz                     the 640 recorded cyipopt MPC calls of sup_learn/*.csv, with the
                                        reconstructed solve inputs and a flag for rows a converged solve of
                                        the reference NLP reproduces (<1e-6)
-  g3_synthetic_{modi,sig_step}.npz     random 5-obstacle scenes solved to a tight KKT point by two scipy
+  g3_synthetic_{modi,sig_step,dd}.npz  random 5-obstacle scenes solved to a tight KKT point by two scipy
                                        methods on the reference callbacks; kept where both agree
   g4_aux.npz                           get_next_states, xk_track_det, alip_des_vel, cal_foot_with_veldes,
                                        constant matrices A, B, W, M_A, M_B, dx_du, dP_du
@@ -488,6 +488,49 @@ def gen_g3_synthetic(modi, sig, rand_obs, n_cases, variant):
     print(f"g3 synthetic {variant}: {n_cases} scenes, both scipy methods agree <1e-8 on {kept}")
 
 
+def gen_g3_synthetic_dd(dd, rand_obs, n_cases):
+    """DD (unicycle) scenes solved by SLSQP and trust-constr on the reference DD callbacks, with the
+    reference's variable bounds v in [0.4, 0.8], w in [-pi/16, pi/16] (MPC_DD_sig_step.py:123-193)."""
+    rng = np.random.default_rng(779)
+    margin = [-0.5, 10.5]
+    R = {k: [] for k in ["x0", "goal", "cir", "nc", "elp", "ne", "u0", "last_u", "u_ref", "agree", "viol",
+                         "f_ref"]}
+    kept = 0
+    for t in range(n_cases):
+        cir, elp = sample_scene(rand_obs, 4000 + t, 5, "cir" if t % 3 else "mix")
+        cs, es = inflate(cir, elp)
+        p0, _ = sample_state(rng, cs, es)
+        x0 = np.array([p0[0], p0[1], p0[4]])
+        last_u = np.array([rng.uniform(0.45, 0.75), rng.uniform(-0.15, 0.15)])
+        u0 = np.tile(last_u, 3)
+        goal = [[10.0, 10.0]]
+        res = []
+        for fn in (solve_slsqp, solve_trust):
+            _StubProblem.solver = _wrap_solver(lambda P, fn=fn: fn(P.problem_obj, P.u0, P.cl, P.cu,
+                                                                    np.asarray(P.lb, float), np.asarray(P.ub, float)))
+            mpc = dd.MPCCBF(goal, cir, cs, elp, es, margin)
+            import contextlib, io
+            with contextlib.redirect_stdout(io.StringIO()):
+                mpc.gen_dd_control(x0, u0, last_u)
+            P = _StubProblem.last
+            u = _last_solution[0].copy()
+            c = np.asarray(P.problem_obj.constraints(u), float)
+            vb = max(0.0, float(np.max(np.concatenate([np.asarray(P.lb) - u, u - np.asarray(P.ub)]))))
+            res.append((u, max(violation(c, P.cl, P.cu), vb), float(P.problem_obj.objective(u))))
+        _StubProblem.solver = None
+        (ua, va, fa), (ub_, vb_, fb) = res
+        agree = float(np.max(np.abs(ua - ub_)))
+        R["x0"].append(x0); R["goal"].append(np.array([10.0, 10.0]))
+        R["cir"].append(_pad(cs, 6, 3)); R["nc"].append(len(cs))
+        R["elp"].append(_pad(es, 6, 5)); R["ne"].append(len(es))
+        R["u0"].append(u0); R["last_u"].append(last_u); R["u_ref"].append(ua)
+        R["agree"].append(agree); R["viol"].append(max(va, vb_)); R["f_ref"].append(fa)
+        if agree < 1e-8 and max(va, vb_) < 1e-8:
+            kept += 1
+    np.savez_compressed(os.path.join(OUT, "g3_synthetic_dd.npz"), **{k: np.asarray(v) for k, v in R.items()})
+    print(f"g3 synthetic dd: {n_cases} scenes, both scipy methods agree <1e-8 on {kept}")
+
+
 # ----------------------------------------------------------------------------------------------
 def gen_g4(modi, sig):
     rng = np.random.default_rng(99)
@@ -546,6 +589,8 @@ def main():
     if not only or "g3y" in only:
         gen_g3_synthetic(modi, sig, rand_obs, 16 if a.quick else 48, "modi")
         gen_g3_synthetic(modi, sig, rand_obs, 16 if a.quick else 48, "sig_step")
+    if not only or "g3dd" in only:
+        gen_g3_synthetic_dd(dd, rand_obs, 16 if a.quick else 48)
     return 0
 
 
