@@ -150,7 +150,7 @@ class Solver:
         x0 = np.ascontiguousarray(x0, np.float64).reshape(-1, self.sdim)
         B = x0.shape[0]
         goal = np.ascontiguousarray(np.broadcast_to(np.asarray(goal, np.float64), (B, 2)))
-        leg = np.ascontiguousarray(np.broadcast_to(np.asarray(leg), (B,)), np.int8)
+        leg = None if leg is None else np.ascontiguousarray(np.broadcast_to(np.asarray(leg), (B,)), np.int8)
         cir = np.ascontiguousarray(np.broadcast_to(np.asarray(cir, np.float64), (B, cfg.nc_max, 3))) \
             if cfg.nc_max else np.zeros((B, 0, 3))
         nc = np.ascontiguousarray(np.broadcast_to(np.asarray(nc), (B,)), np.int32)
@@ -165,7 +165,7 @@ class Solver:
         """Solve a batch from host arrays; returns a dict of numpy outputs."""
         B, x0, goal, leg, cir, nc, elp, ne = self._inputs(x0, goal, leg, cir, nc, elp, ne)
         u0 = np.ascontiguousarray(u0, np.float64).reshape(B, self.n)
-        lu = None if last_u is None else np.ascontiguousarray(last_u, np.float64).reshape(B, 2)
+        lu = None if last_u is None else np.ascontiguousarray(np.broadcast_to(np.asarray(last_u, np.float64), (B, 2)))
         out = dict(u=np.zeros((B, self.n)), foot=np.zeros((B, 3)), x_pred=np.zeros((B, self.cfg.N, self.sdim)),
                    status=np.zeros(B, np.int32), iters=np.zeros(B, np.int32))
         rc = self._L.alipmpc_solve_batch(self._h, B, _ptr(x0), _ptr(goal), _ptr(leg), _ptr(cir), _ptr(nc), _ptr(elp),
@@ -177,7 +177,7 @@ class Solver:
     def eval(self, x0, goal, leg, cir, nc, elp=None, ne=None, u=None, last_u=None, want_J=True):
         B, x0, goal, leg, cir, nc, elp, ne = self._inputs(x0, goal, leg, cir, nc, elp, ne)
         u = np.ascontiguousarray(u, np.float64).reshape(B, self.n)
-        lu = None if last_u is None else np.ascontiguousarray(last_u, np.float64).reshape(B, 2)
+        lu = None if last_u is None else np.ascontiguousarray(np.broadcast_to(np.asarray(last_u, np.float64), (B, 2)))
         mm = self.m_max
         out = dict(f=np.zeros(B), grad=np.zeros((B, self.n)), c=np.zeros((B, mm)),
                    J=np.zeros((B, mm, self.n)) if want_J else None, cl=np.zeros((B, mm)), cu=np.zeros((B, mm)),

@@ -49,7 +49,7 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 // ------------------------------------------------------------------------------------------------
 struct KP {
     int nc_max, ne_max, rps, m_max, mr4, mo4, modi, max_iter, select_obs, detour;
-    double tol, acc_tol, q, p, r, gm1, s, detect_r2, leg2, bvx_lo, bvx_hi, bvy_lo, bvy_hi, dth, mu_init;
+    double tol, acc_tol, q, p, r, gm1, s, detect_r2, leg2, bvx_lo, bvx_hi, bvy_lo, bvy_hi, dth, mu_init, dt, dd_t;
     const double* G;   // NG x NCP
     const double* E;   // NG x 5
     const double* Gu;  // NG x NCPU : u-parametrisation V = Eu x0 + Gu u (warm start u0 -> p0)
@@ -63,6 +63,7 @@ struct KP {
     const double* elp;
     const int32_t* ne;
     const double* u0;
+    const double* last_u;   // DD: previous control (B x 2)
     // solve outputs
     double* u_out;
     double* foot_out;
@@ -1728,6 +1729,921 @@ __global__ __launch_bounds__(256, 4) void eval_kernel(KP Pv)
     }
 }
 
+// ================================================================================================
+// DD variant: unicycle MPC-CBF (MPC_DD_sig_step.py:123-193 set-up, 320-572 LIP_Prob)
+//   x = [px, py, th], u = [v_0, w_0, ..., v_{N-1}, w_{N-1}] (n = 2N),
+//   x_{i+1} = x_i + [T v_i cos th_i, T v_i sin th_i, w_i].
+// The dynamics are not affine in u, so there is no generator space: each evaluation rolls the N steps
+// out (state lanes, one sincos per lane + readlane prefix sums), every row lane writes its full
+// Jacobian row (n <= 12, closed forms of cal_dx_du :534-566) to LDS, and the exact Hessian adds the
+// rollout's second derivatives.  The interior-point logic (barrier, filter, inertia correction) is the
+// same as solve_kernel's.
+// Solve rows per step: [cbf circle slots, cbf ellipse slots, v + s w <= v_max, v - s w <= v_max,
+// v in [v_min, v_max], w in [-w_max, w_max]] (f_en split and the reference's variable bounds as rows),
+// then N objective pseudo-rows.  Eval rows per step: the reference's [cbf..., f_en = s|w| + v].
+// ================================================================================================
+enum DDType { D_CIR = 0, D_ELP, D_FENP, D_FENM, D_VB, D_WB, D_NONE, D_OBJ, D_FEN };
+enum { DK_GM1 = 0, DK_S, DK_Q, DK_P, DK_R, DK_GX, DK_GY, DK_T, DK_TT, DK_LU0, DK_LU1, DK_THMAX, DK_THMIN,
+       DK_MACT, DK_NBL, DK_TOL, DK_ACCTOL, DK_X0, DK_X1, DK_X2, DK_COUNT };
+constexpr int DD_ST = 8;   // per-step stride of the state table: px, py, th, T cos th, T sin th
+
+template <int N>
+struct DDW {
+    double* cst;   // DK_COUNT (rounded to 24)
+    double* STa;   // (N+1) x DD_ST  state tables (current / trial swap roles)
+    double* STb;
+    double* Ua;    // 16 decision (current / trial)
+    double* Ub;
+    double* dU;    // 16 step
+    double* Jd;    // mo4 x 16 Jacobian rows
+    double* ry;    // mo4
+    double* rsig;  // mo4
+    double* rw;    // mo4
+    double* hl;    // (N+1) x 8: Hessian parts per step [h00 h01 h11 h02 h12 h22 g0 g1]
+    double* hobj;  // (N+1) x 8: objective contributions (written by the OBJ rows)
+    double* obs6;  // (nobs + 1) x 6
+    double* K;     // 16 x 17
+    double* rclo;  // mo4
+    double* rcuo;  // mo4
+};
+
+template <int N>
+__host__ __device__ constexpr int ddw_doubles(int nobs, int mo4)
+{
+    int d = 24 + 2 * (N + 1) * DD_ST + 3 * 16 + 16 * mo4 + 3 * mo4 + 2 * 8 * (N + 1) + 6 * (nobs + 1) + 16 * 17 +
+            2 * mo4;
+    return (d + 3) & ~3;
+}
+
+template <int N>
+__device__ DDW<N> carve_dd(double* p, int nobs, int mo4)
+{
+    DDW<N> w;
+    w.Jd = p; p += 16 * mo4;   // first: 32-byte aligned
+    w.cst = p; p += 24;
+    w.STa = p; p += (N + 1) * DD_ST;
+    w.STb = p; p += (N + 1) * DD_ST;
+    w.Ua = p; p += 16;
+    w.Ub = p; p += 16;
+    w.dU = p; p += 16;
+    w.ry = p; p += mo4;
+    w.rsig = p; p += mo4;
+    w.rw = p; p += mo4;
+    w.hl = p; p += 8 * (N + 1);
+    w.hobj = p; p += 8 * (N + 1);
+    w.obs6 = p; p += 6 * (nobs + 1);
+    w.K = p; p += 16 * 17;
+    w.rclo = p; p += mo4;
+    w.rcuo = p;
+    return w;
+}
+
+// row decode (solve layout split = true: rps = nobs + 4; eval layout: rps = nobs + 1)
+__device__ __forceinline__ void dd_decode(int r, int rps, int m, int nc_max, int ne_max, int nc, int ne, bool split,
+                                          int& type, int& k, int& oi)
+{
+    type = D_NONE;
+    k = 0;
+    oi = 0;
+    if (r >= m) return;
+    k = r / rps;
+    const int l = r - k * rps;
+    const int nobs = nc_max + ne_max;
+    if (l < nc_max) {
+        type = l < nc ? D_CIR : D_NONE;
+        oi = l;
+    } else if (l < nobs) {
+        type = (l - nc_max) < ne ? D_ELP : D_NONE;
+        oi = l;
+    } else if (!split) {
+        type = D_FEN;
+    } else {
+        type = l == nobs ? D_FENP : l == nobs + 1 ? D_FENM : l == nobs + 2 ? D_VB : D_WB;
+    }
+}
+
+__device__ __forceinline__ void dd_bounds(const KP& P, int type, double& cl, double& cu)
+{
+    switch (type) {
+    case D_CIR:
+    case D_ELP: cl = 0.0; cu = INFINITY; break;
+    case D_FENP:
+    case D_FENM: cl = -INFINITY; cu = P.bvx_hi; break;
+    case D_FEN:
+    case D_VB: cl = P.bvx_lo; cu = P.bvx_hi; break;
+    case D_WB: cl = -P.dth; cu = P.dth; break;
+    default: cl = -INFINITY; cu = INFINITY;
+    }
+}
+
+// state lanes k = 0..N roll the unicycle out from x0 with decision U (LDS) into ST
+template <int N>
+__device__ void dd_rollout(const double* cst, const double* U, double* ST, int lane)
+{
+    const double T = cst[DK_T];
+    double th = cst[DK_X2];
+#pragma unroll
+    for (int j = 0; j < N; ++j) th += j < lane ? U[2 * j + 1] : 0.0;
+    double sn, cs;
+    sincos(th, &sn, &cs);
+    const double tc = T * cs, ts = T * sn;
+    const double v = lane < N ? U[2 * (lane < N ? lane : 0)] : 0.0;
+    const double ax = tc * v, ay = ts * v;
+    double px = cst[DK_X0], py = cst[DK_X1];
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        const double a = bcast(ax, j), b = bcast(ay, j);
+        px += j < lane ? a : 0.0;
+        py += j < lane ? b : 0.0;
+    }
+    if (lane <= N) {
+        double* s = ST + DD_ST * lane;
+        s[0] = px; s[1] = py; s[2] = th; s[3] = tc; s[4] = ts;
+    }
+}
+
+// column j pair (v_j, w_j) of d(px, py)_k / du for a lane-varying step k (rows of cal_dx_du :534-566):
+//   d px_k / d v_j = T cos th_j,  d py_k / d v_j = T sin th_j,  d px_k / d w_j = -(py_k - py_{j+1}),
+//   d py_k / d w_j = px_k - px_{j+1},  d th_k / d w_j = 1   (all for j < k, else 0)
+struct DDCol {
+    double xv, yv, xw, yw, tw;
+};
+__device__ __forceinline__ DDCol dd_col(const double* ST, int j, int k, double pxk, double pyk)
+{
+    const double* s = ST + DD_ST * j;
+    const double* s1 = ST + DD_ST * (j + 1);
+    const bool in = j < k;
+    DDCol c;
+    c.xv = in ? s[3] : 0.0;
+    c.yv = in ? s[4] : 0.0;
+    c.xw = in ? -(pyk - s1[1]) : 0.0;
+    c.yw = in ? (pxk - s1[0]) : 0.0;
+    c.tw = in ? 1.0 : 0.0;
+    return c;
+}
+
+// value of DD row `type` at (ST, U); JAC: its Jacobian row is written to Jout[0..n-1] (OBJ rows also
+// return their local Hessian parts in hx)
+template <int N, bool JAC>
+__device__ double dd_row(int type, int k, const double (&o)[6], const double* cst, const double* ST,
+                         const double* U, double* Jout, double (&hx)[8])
+{
+    constexpr int n = 2 * N;
+    const double gm1 = cst[DK_GM1], sfen = cst[DK_S];
+    double c = 0.0;
+    if (type == D_CIR || type == D_ELP) {
+        const double* s1 = ST + DD_ST * (k + 1);
+        const double* s0 = ST + DD_ST * k;
+        const double x1 = s1[0] - o[0], y1 = s1[1] - o[1], x0 = s0[0] - o[0], y0 = s0[1] - o[1];
+        c = (o[2] * x1 * x1 + o[3] * x1 * y1 + o[4] * y1 * y1 - o[5]) +
+            gm1 * (o[2] * x0 * x0 + o[3] * x0 * y0 + o[4] * y0 * y0 - o[5]);
+        if (JAC) {
+            const double g1x = 2 * o[2] * x1 + o[3] * y1, g1y = 2 * o[4] * y1 + o[3] * x1;
+            const double g0x = gm1 * (2 * o[2] * x0 + o[3] * y0), g0y = gm1 * (2 * o[4] * y0 + o[3] * x0);
+#pragma unroll
+            for (int j = 0; j < N; ++j) {
+                const DDCol a1 = dd_col(ST, j, k + 1, s1[0], s1[1]);
+                const DDCol a0 = dd_col(ST, j, k, s0[0], s0[1]);
+                Jout[2 * j] = g1x * a1.xv + g1y * a1.yv + g0x * a0.xv + g0y * a0.yv;
+                Jout[2 * j + 1] = g1x * a1.xw + g1y * a1.yw + g0x * a0.xw + g0y * a0.yw;
+            }
+        }
+    } else if (type == D_OBJ) {
+        const double* sk = ST + DD_ST * k;
+        const double w = cst[DK_Q] + (k == 1 ? cst[DK_P] : 0.0), r = cst[DK_R], t = cst[DK_TT];
+        const double dxg = cst[DK_GX] - sk[0], dyg = cst[DK_GY] - sk[1];
+        const double phi = sk[2] - atan2(dyg, dxg);
+        const double up0 = k >= 2 ? U[2 * k - 4] : cst[DK_LU0], up1 = k >= 2 ? U[2 * k - 3] : cst[DK_LU1];
+        const double d0 = U[2 * k - 2] - up0, d1 = U[2 * k - 1] - up1;
+        c = w * (dxg * dxg + dyg * dyg) + r * phi * phi + t * (d0 * d0 + d1 * d1);
+        if (JAC) {
+            const double rho2 = dxg * dxg + dyg * dyg, ir2 = 1.0 / rho2;
+            const double gp0 = -dyg * ir2, gp1 = dxg * ir2;
+            const double ax = -2 * w * dxg + 2 * r * phi * gp0, ay = -2 * w * dyg + 2 * r * phi * gp1, at = 2 * r * phi;
+#pragma unroll
+            for (int j = 0; j < N; ++j) {
+                const DDCol a = dd_col(ST, j, k, sk[0], sk[1]);
+                const double sm = j == k - 1 ? 2 * t : (j == k - 2 ? -2 * t : 0.0);
+                Jout[2 * j] = ax * a.xv + ay * a.yv + sm * d0;
+                Jout[2 * j + 1] = ax * a.xw + ay * a.yw + at * a.tw + sm * d1;
+            }
+            const double ir4 = ir2 * ir2;
+            const double s00 = 2 * dxg * dyg * ir4, s01 = (dyg * dyg - dxg * dxg) * ir4, s11 = -2 * dxg * dyg * ir4;
+            hx[0] = 2 * w + 2 * r * (gp0 * gp0 - phi * s00);
+            hx[1] = 2 * r * (gp0 * gp1 - phi * s01);
+            hx[2] = 2 * w + 2 * r * (gp1 * gp1 - phi * s11);
+            hx[3] = 2 * r * gp0;
+            hx[4] = 2 * r * gp1;
+            hx[5] = 2 * r;
+            hx[6] = ax;
+            hx[7] = ay;
+        }
+    } else if (type != D_NONE) {
+        const double v = U[2 * k], wv = U[2 * k + 1];
+        double jv = 1.0, jw = 0.0;
+        switch (type) {
+        case D_FENP: c = v + sfen * wv; jw = sfen; break;
+        case D_FENM: c = v - sfen * wv; jw = -sfen; break;
+        case D_VB: c = v; break;
+        case D_WB: c = wv; jv = 0.0; jw = 1.0; break;
+        case D_FEN: c = sfen * fabs(wv) + v; jw = sfen * (wv == 0.0 ? 0.0 : copysign(1.0, wv)); break;   // den_du
+        default: break;
+        }
+        if (JAC) {
+#pragma unroll
+            for (int a = 0; a < n; ++a) Jout[a] = a == 2 * k ? jv : (a == 2 * k + 1 ? jw : 0.0);
+        }
+    } else if (JAC) {
+#pragma unroll
+        for (int a = 0; a < n; ++a) Jout[a] = 0.0;
+    }
+    return c;
+}
+
+// DD prologue: inputs, obstacle forms, constants; returns the number of valid circles / ellipses
+template <int N>
+__device__ void dd_prologue(const KP& P, const DDW<N>& w, long long b, int lane, int nc_max, int ne_max, int& ncv,
+                            int& nev)
+{
+    constexpr int n = 2 * N;
+    const double* x0 = P.x0 + 3 * b;
+    ncv = min(P.nc[b], nc_max);
+    nev = P.ne ? min(P.ne[b], ne_max) : 0;
+    const int nobs = nc_max + ne_max;
+    for (int j = lane; j <= nobs; j += WAVE) {
+        double o[6] = {0, 0, 0, 0, 0, 0};
+        if (j < nc_max) {
+            if (j < ncv) {
+                const double* c = P.cir + ((size_t)b * nc_max + j) * 3;
+                o[0] = c[0]; o[1] = c[1]; o[2] = 1.0; o[4] = 1.0; o[5] = c[2] * c[2];
+            }
+        } else if (j < nobs) {
+            const int e = j - nc_max;
+            if (e < nev) {
+                const double* el = P.elp + ((size_t)b * ne_max + e) * 5;
+                double se, ce;
+                sincos(el[4], &se, &ce);
+                o[0] = el[0]; o[1] = el[1];
+                o[2] = (el[3] * ce) * (el[3] * ce) + (el[2] * se) * (el[2] * se);
+                o[3] = 2 * ce * se * (el[3] * el[3] - el[2] * el[2]);
+                o[4] = (el[3] * se) * (el[3] * se) + (el[2] * ce) * (el[2] * ce);
+                o[5] = (el[3] * el[2]) * (el[3] * el[2]);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 6; ++i) w.obs6[6 * j + i] = o[i];
+    }
+    if (lane == 0) {
+        w.cst[DK_GM1] = P.gm1; w.cst[DK_S] = P.s; w.cst[DK_Q] = P.q; w.cst[DK_P] = P.p; w.cst[DK_R] = P.r;
+        w.cst[DK_GX] = P.goal[2 * b]; w.cst[DK_GY] = P.goal[2 * b + 1]; w.cst[DK_T] = P.dt; w.cst[DK_TT] = P.dd_t;
+        w.cst[DK_LU0] = P.last_u ? P.last_u[2 * b] : 0.0; w.cst[DK_LU1] = P.last_u ? P.last_u[2 * b + 1] : 0.0;
+        w.cst[DK_TOL] = P.tol; w.cst[DK_ACCTOL] = P.acc_tol;
+        w.cst[DK_X0] = x0[0]; w.cst[DK_X1] = x0[1]; w.cst[DK_X2] = x0[2];
+    }
+    if (lane < 16) w.Ua[lane] = lane < n ? P.u0[(size_t)b * n + lane] : 0.0;
+    wave_sync();
+}
+
+// Hessian parts per step k (lane k = 1..N): objective parts from the OBJ rows + D-CBF rows of steps k-1
+// (post-step state) and k (pre-step state, gamma - 1 factor)
+template <int N>
+__device__ void dd_hess_steps(const DDW<N>& w, const double* ST, int lane, int rps, int nobs)
+{
+    if (lane < 1 || lane > N) return;
+    const int k = lane;
+    const double* ho = w.hobj + 8 * k;
+    double h00 = ho[0], h01 = ho[1], h11 = ho[2], h02 = ho[3], h12 = ho[4], h22 = ho[5], g0 = ho[6], g1 = ho[7];
+    const double px = ST[DD_ST * k], py = ST[DD_ST * k + 1], gm1 = w.cst[DK_GM1];
+#pragma unroll 4
+    for (int j = 0; j < nobs; ++j) {
+        const double* o = w.obs6 + 6 * j;
+        const double x = px - o[0], y = py - o[1];
+        const double dx = 2 * o[2] * x + o[3] * y, dy = 2 * o[4] * y + o[3] * x;
+        double y1 = w.ry[(k - 1) * rps + j];
+        double y0 = k < N ? w.ry[k * rps + j] * gm1 : 0.0;
+        const double yy = y1 + y0;
+        h00 -= yy * 2 * o[2];
+        h01 -= yy * o[3];
+        h11 -= yy * 2 * o[4];
+        g0 -= yy * dx;
+        g1 -= yy * dy;
+    }
+    double* hl = w.hl + 8 * k;
+    hl[0] = h00; hl[1] = h01; hl[2] = h11; hl[3] = h02; hl[4] = h12; hl[5] = h22; hl[6] = g0; hl[7] = g1;
+}
+
+// exact Hessian entry H[a][b] (rollout second derivatives included) + smoothness term
+template <int N>
+__device__ double dd_hess_entry(const DDW<N>& w, const double* ST, int a, int b)
+{
+    const double T = w.cst[DK_T], t = w.cst[DK_TT];
+    const int ja = a >> 1, jb = b >> 1;
+    const bool va = (a & 1) == 0, vb = (b & 1) == 0;
+    double h = 0.0;
+#pragma unroll
+    for (int k = 1; k <= N; ++k) {
+        const double* sk = ST + DD_ST * k;
+        const double* hl = w.hl + 8 * k;
+        // d(px, py, th)_k / du_a and / du_b
+        double xa, ya, ta, xb, yb, tb;
+        {
+            const double* s = ST + DD_ST * ja;
+            const double* s1 = ST + DD_ST * (ja + 1);
+            const bool in = ja < k;
+            xa = in ? (va ? s[3] : -(sk[1] - s1[1])) : 0.0;
+            ya = in ? (va ? s[4] : (sk[0] - s1[0])) : 0.0;
+            ta = (in && !va) ? 1.0 : 0.0;
+        }
+        {
+            const double* s = ST + DD_ST * jb;
+            const double* s1 = ST + DD_ST * (jb + 1);
+            const bool in = jb < k;
+            xb = in ? (vb ? s[3] : -(sk[1] - s1[1])) : 0.0;
+            yb = in ? (vb ? s[4] : (sk[0] - s1[0])) : 0.0;
+            tb = (in && !vb) ? 1.0 : 0.0;
+        }
+        h += xa * (hl[0] * xb + hl[1] * yb + hl[3] * tb) + ya * (hl[1] * xb + hl[2] * yb + hl[4] * tb) +
+             ta * (hl[3] * xb + hl[4] * yb + hl[5] * tb);
+        // second derivatives of px_k, py_k
+        double sxx = 0.0, syy = 0.0;
+        if (va != vb) {
+            const int jv = va ? ja : jb, jw = va ? jb : ja;   // d2 / dv_jv dw_jw, jw < jv < k
+            if (jw < jv && jv < k) {
+                sxx = -ST[DD_ST * jv + 4];
+                syy = ST[DD_ST * jv + 3];
+            }
+        } else if (!va) {
+            const int mm = ja > jb ? ja : jb;
+            if (mm < k) {
+                sxx = -(sk[0] - ST[DD_ST * (mm + 1)]);
+                syy = -(sk[1] - ST[DD_ST * (mm + 1) + 1]);
+            }
+        }
+        h += hl[6] * sxx + hl[7] * syy;
+    }
+    if (a == b) h += 2 * t * (ja < N - 1 ? 2.0 : 1.0);
+    if ((a & 1) == (b & 1) && (ja - jb == 1 || jb - ja == 1)) h -= 2 * t;
+    return h;
+}
+
+// ------------------------------------------------------------------------------------------------
+// DD solve kernel (one instance per wave); RPL row groups of 64 lanes, KSM = 16 RPL J-layout steps
+// ------------------------------------------------------------------------------------------------
+template <int N, int RPL>
+__global__ __launch_bounds__(256, 4) void dd_solve_kernel(KP Pv)
+{
+    constexpr int n = 2 * N;
+    constexpr int KSM = 16 * RPL;
+    constexpr int KLD = 17;
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    KP* Ps = reinterpret_cast<KP*>(smem);
+    double* wsb = smem + KP_DOUBLES;
+    if (threadIdx.x == 0) *Ps = Pv;
+    __syncthreads();
+    const KP& P = *Ps;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
+    int lane = lane_id();
+    const long long b = (long long)blockIdx.x * WAVES_PER_BLOCK + wv;
+    if (b >= P.B) return;
+    const int mr4 = rfl(P.mr4), mo4 = rfl(P.mo4), m_max = rfl(P.m_max), rps = rfl(P.rps);
+    const int nc_max = rfl(P.nc_max), ne_max = rfl(P.ne_max), nobs = nc_max + ne_max, max_iter = rfl(P.max_iter);
+    DDW<N> w = carve_dd<N>(wsb + (size_t)wv * ddw_doubles<N>(nobs, mo4), nobs, mo4);
+    int ncv, nev;
+    dd_prologue<N>(P, w, b, lane, nc_max, ne_max, ncv, nev);
+    double* ST = w.STa;   // current point
+    double* STt = w.STb;  // trial point
+    double* U = w.Ua;
+    double* Ut = w.Ub;
+    dd_rollout<N>(w.cst, U, ST, lane);
+    for (int i = lane; i < 16 * mo4; i += WAVE) w.Jd[i] = 0.0;
+    wave_sync();
+    int g4 = lane >> 4, col = lane & 15;
+#define HL(q) (cl[q] != -INFINITY)
+#define HU(q) (cu[q] != INFINITY)
+#define RELANE()                           \
+    do {                                   \
+        RELAUNDER(lane);                   \
+        g4 = lane >> 4;                    \
+        col = lane & 15;                   \
+        for (int q_ = 0; q_ < RPL; ++q_) { \
+            RELAUNDER(rtype[q_]);          \
+            RELAUNDER(rk[q_]);             \
+            RELAUNDER(roi[q_]);            \
+            RELAUNDER(cl[q_]);             \
+            RELAUNDER(cu[q_]);             \
+        }                                  \
+    } while (0)
+    int rtype[RPL], rk[RPL], roi[RPL];
+    double cl[RPL], cu[RPL], cr[RPL], sr[RPL], zl[RPL], zu[RPL], idl[RPL], idu[RPL];
+    double mu = uni(P.mu_init);
+    double th0 = 0.0, nbl = 0.0, mal = 0.0, fo = 0.0, lg0 = 0.0;
+    double hx[8];
+#pragma unroll
+    for (int q = 0; q < RPL; ++q) {
+        const int r = lane + WAVE * q;
+        int t, k, oi;
+        dd_decode(r, rps, m_max, nc_max, ne_max, ncv, nev, true, t, k, oi);
+        if (r >= mr4 && r < mr4 + N) {
+            t = D_OBJ;
+            k = r - mr4 + 1;
+        }
+        rtype[q] = t;
+        rk[q] = k;
+        roi[q] = oi;
+        double clo, cuo;
+        dd_bounds(P, t, clo, cuo);
+        if (r < mr4) {
+            w.rclo[r] = clo;
+            w.rcuo[r] = cuo;
+        }
+        nbl += (double)isfinite(clo) + (double)isfinite(cuo);
+        mal += t < D_NONE ? 1.0 : 0.0;
+        cl[q] = isfinite(clo) ? clo - 1e-8 * fmax(1.0, fabs(clo)) : -INFINITY;
+        cu[q] = isfinite(cuo) ? cuo + 1e-8 * fmax(1.0, fabs(cuo)) : INFINITY;
+        double o[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) o[i] = w.obs6[6 * oi + i];
+        cr[q] = dd_row<N, false>(t, k, o, w.cst, ST, U, nullptr, hx);
+        double v = cr[q];
+        const double pl = HL(q) ? fmin(1e-2 * fmax(1.0, fabs(cl[q])), 1e-2 * (cu[q] - cl[q])) : 0.0;
+        const double pu = HU(q) ? fmin(1e-2 * fmax(1.0, fabs(cu[q])), 1e-2 * (cu[q] - cl[q])) : 0.0;
+        if (HL(q) && HU(q))
+            v = fmin(fmax(v, cl[q] + pl), cu[q] - pu);
+        else if (HL(q))
+            v = fmax(v, cl[q] + pl);
+        else if (HU(q))
+            v = fmin(v, cu[q] - pu);
+        sr[q] = t < D_NONE ? v : 0.0;
+        zl[q] = HL(q) ? 1.0 : 0.0;
+        zu[q] = HU(q) ? 1.0 : 0.0;
+        const double dl = sr[q] - cl[q], du = cu[q] - sr[q];
+        idl[q] = HL(q) ? rcp_nr(dl) : 0.0;
+        idu[q] = HU(q) ? rcp_nr(du) : 0.0;
+        lg0 += HL(q) ? (HU(q) ? log(dl * du) : log(dl)) : (HU(q) ? log(du) : 0.0);
+        if (t < D_NONE) th0 += fabs(cr[q] - sr[q]);
+        if (t == D_OBJ) fo += cr[q];
+    }
+    wsum2(th0, nbl);
+    wsum2(fo, lg0);
+    mal = wsum(mal);
+    double f_cur = fo, lsum_cur = lg0;
+    if (lane == 0) {
+        w.cst[DK_THMAX] = 1e4 * fmax(1.0, th0);
+        w.cst[DK_THMIN] = 1e-4 * fmax(1.0, th0);
+        w.cst[DK_MACT] = mal;
+        w.cst[DK_NBL] = nbl;
+    }
+    wave_sync();
+    double fth0 = INFINITY, fph0 = INFINITY, fth1 = INFINITY, fph1 = INFINITY;
+    int nf = 0;
+    double dw_last = 0.0;
+    int status = -1, it = 0, n_rest = 0;
+    double e0 = INFINITY;
+    const double gth = 1e-5, gph = 1e-8, sth = 1.1, sph = 2.3, eta = 1e-8, gal = 0.05;
+
+    for (it = 0; it <= max_iter; ++it) {
+        // ---- row layout: Jacobian rows at the current point (OBJ rows: grad f_k + Hessian parts)
+        RELANE();
+#pragma unroll
+        for (int q = 0; q < RPL; ++q) {
+            const int r = lane + WAVE * q;
+            double o[6];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) o[i] = w.obs6[6 * roi[q] + i];
+            // every lane owns a row (mo4 = 64 RPL); columns n..15 stay zero (zeroed in the prologue)
+            dd_row<N, true>(rtype[q], rk[q], o, w.cst, ST, U, w.Jd + 16 * r, hx);
+            w.ry[r] = rtype[q] == D_OBJ ? -1.0 : zl[q] - zu[q];
+            if (rtype[q] == D_OBJ) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) w.hobj[8 * rk[q] + i] = hx[i];
+            }
+        }
+        wave_sync();
+        // ---- J layout: gl = J^T y - grad f
+        RELANE();
+        double gl = 0.0;
+#pragma unroll
+        for (int s = 0; s < KSM; ++s) {
+            const int r = 4 * s + g4;
+            gl += w.Jd[16 * r + col] * w.ry[r];
+        }
+        gl = gsum(gl);
+        // ---- convergence test and barrier update
+        double ru = (g4 == 0 && col < n) ? fabs(gl) : 0.0;
+        double rcm = 0.0, nz = 0.0, comp0 = 0.0;
+#pragma unroll
+        for (int q = 0; q < RPL; ++q) {
+            const double dl = sr[q] - cl[q], du = cu[q] - sr[q];
+            if (rtype[q] < D_NONE) rcm = fmax(rcm, fabs(cr[q] - sr[q]));
+            nz += fabs(zl[q]) + fabs(zu[q]);
+            if (HL(q)) comp0 = fmax(comp0, fabs(dl * zl[q]));
+            if (HU(q)) comp0 = fmax(comp0, fabs(du * zu[q]));
+        }
+        ru = wmax(ru);
+        rcm = wmax(rcm);
+        nz = wsum(nz);
+        comp0 = wmax(comp0);
+        const double sd = uni(fmax(100.0, nz / (w.cst[DK_MACT] + n)) / 100.0);
+        const double sc = uni(fmax(100.0, nz / fmax(1.0, w.cst[DK_NBL])) / 100.0);
+        const double base_err = uni(fmax(ru / sd, rcm));
+        e0 = uni(fmax(base_err, comp0 / sc));
+        if (e0 <= w.cst[DK_TOL]) {
+            status = 0;
+            break;
+        }
+        if (it == max_iter) break;
+        {
+            const double mu_min = w.cst[DK_TOL] / 10.0;
+            const double mu_prev = mu;
+            for (int t = 0; t < 8; ++t) {
+                double cm = 0.0;
+#pragma unroll
+                for (int q = 0; q < RPL; ++q) {
+                    const double dl = sr[q] - cl[q], du = cu[q] - sr[q];
+                    if (HL(q)) cm = fmax(cm, fabs(dl * zl[q] - mu));
+                    if (HU(q)) cm = fmax(cm, fabs(du * zu[q] - mu));
+                }
+                cm = wmax(cm);
+                if (fmax(base_err, cm / sc) <= 10.0 * mu && mu > mu_min)
+                    mu = uni(fmax(mu_min, fmin(0.2 * mu, mu * sqrt(mu))));
+                else
+                    break;
+            }
+            if (mu != mu_prev) nf = 0;
+        }
+        const double tau = uni(fmax(0.99, 1.0 - mu));
+        // ---- Sigma, rhs weights, Hessian parts
+        RELANE();
+        double rcv[RPL];
+#pragma unroll
+        for (int q = 0; q < RPL; ++q) {
+            const int r = lane + WAVE * q;
+            const double sg = zl[q] * idl[q] + zu[q] * idu[q];
+            rcv[q] = rtype[q] < D_NONE ? cr[q] - sr[q] : 0.0;
+            double wr = mu * idl[q] - mu * idu[q] - sg * rcv[q];
+            wr = rtype[q] == D_OBJ ? -1.0 : wr;
+            if (r < mo4) {
+                w.rsig[r] = sg;
+                w.rw[r] = wr;
+            }
+        }
+        dd_hess_steps<N>(w, ST, lane, rps, nobs);
+        wave_sync();
+        // ---- K = J^T Sigma J (MFMA) + exact Hessian, rhs = J^T w - grad f
+        RELANE();
+        double rhs;
+        {
+            d4 acc0 = d4{0.0, 0.0, 0.0, 0.0}, acc1 = d4{0.0, 0.0, 0.0, 0.0};
+            double pw = 0.0;
+#pragma unroll
+            for (int s = 0; s < KSM; ++s) {
+                const int r = 4 * s + g4;
+                const double j = w.Jd[16 * r + col];
+                const double sg = w.rsig[r];
+                pw += j * w.rw[r];
+                if (s & 1)
+                    acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(j, sg * j, acc1, 0, 0, 0);
+                else
+                    acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(j, sg * j, acc0, 0, 0, 0);
+            }
+            rhs = gsum(pw);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) w.K[(g4 + 4 * i) * KLD + col] = acc0[i] + acc1[i];
+        }
+        wave_sync();
+        for (int e = lane; e < n * n; e += WAVE) {
+            const int a = e / n, bb = e - a * n;
+            w.K[a * KLD + bb] += dd_hess_entry<N>(w, ST, a, bb);
+        }
+        wave_sync();
+        // ---- factor with inertia correction, solve for du
+        RELANE();
+        double xv;
+        {
+            const double rhs_l = lane < n ? rhs : 0.0;
+            double a[n];
+            double myidg = 1.0;
+#pragma unroll
+            for (int j = 0; j < n; ++j) a[j] = lane < n ? w.K[lane * KLD + j] : (lane == j ? 1.0 : 0.0);
+            if (!chol_rows<n>(a, myidg, lane)) {
+                double dw = dw_last == 0.0 ? 1e-4 : fmax(1e-20, dw_last / 3.0);
+                for (;;) {
+#pragma unroll
+                    for (int j = 0; j < n; ++j)
+                        a[j] = (lane < n ? w.K[lane * KLD + j] : (lane == j ? 1.0 : 0.0)) + (lane == j ? dw : 0.0);
+                    if (chol_rows<n>(a, myidg, lane)) break;
+                    dw *= dw_last == 0.0 ? 100.0 : 8.0;
+                    if (dw > 1e40) break;
+                }
+                dw_last = uni(dw);
+            }
+            double acc = 0.0, yv = 0.0;
+#pragma unroll
+            for (int k = 0; k < n; ++k) {
+                const double yk = bcast((rhs_l - acc) * myidg, k);
+                yv = lane == k ? yk : yv;
+                acc += lane > k ? a[k] * yk : 0.0;
+            }
+            wave_sync();
+            if (lane < n) {
+#pragma unroll
+                for (int j = 0; j < n; ++j) w.K[lane * KLD + j] = j <= lane ? a[j] : 0.0;
+            }
+            wave_sync();
+            acc = 0.0;
+            xv = 0.0;
+#pragma unroll
+            for (int i = n - 1; i >= 0; --i) {
+                const double xi = bcast((yv - acc) * myidg, i);
+                xv = lane == i ? xi : xv;
+                acc += lane < i ? w.K[i * KLD + (lane & 15)] * xi : 0.0;
+            }
+        }
+        if (lane < 16) w.dU[lane] = lane < n ? xv : 0.0;
+        wave_sync();
+        // ---- slack / multiplier steps, fraction to boundary
+        RELANE();
+        double dS[RPL], dZl[RPL], dZu[RPL];
+        double ap = 1.0, az = 1.0, theta = 0.0, sl = 0.0, gdv = 0.0;
+#pragma unroll
+        for (int q = 0; q < RPL; ++q) {
+            const int r = lane + WAVE * q;
+            double jd = 0.0;
+            if (r < mo4) {
+#pragma unroll
+                for (int a = 0; a < n; ++a) jd += w.Jd[16 * r + a] * w.dU[a];
+            }
+            if (rtype[q] == D_OBJ) gdv += jd;
+            dS[q] = rtype[q] < D_NONE ? jd + rcv[q] : 0.0;
+            dZl[q] = HL(q) ? mu * idl[q] - zl[q] - zl[q] * idl[q] * dS[q] : 0.0;
+            dZu[q] = HU(q) ? mu * idu[q] - zu[q] + zu[q] * idu[q] * dS[q] : 0.0;
+            const double dl = sr[q] - cl[q], du = cu[q] - sr[q];
+            const double ids = rcp_nr(dS[q]);
+            if (HL(q) && dS[q] < 0) ap = fmin(ap, -tau * dl * ids);
+            if (HU(q) && dS[q] > 0) ap = fmin(ap, tau * du * ids);
+            if (HL(q) && dZl[q] < 0) az = fmin(az, -tau * zl[q] * rcp_nr(dZl[q]));
+            if (HU(q) && dZu[q] < 0) az = fmin(az, -tau * zu[q] * rcp_nr(dZu[q]));
+            theta += fabs(rcv[q]);
+            sl += (HL(q) ? dS[q] * idl[q] : 0.0) - (HU(q) ? dS[q] * idu[q] : 0.0);
+        }
+        ap = wmin(ap);
+        az = wmin(az);
+        wsum2(theta, gdv);
+        sl = wsum(sl);
+        const double phi = uni(f_cur - mu * lsum_cur);
+        const double gphi = uni(gdv - mu * sl);
+        const double lsw = uni(gphi < 0 ? sth * log(theta) - sph * log(-gphi) : 0.0);
+        double amin;
+        if (gphi < 0) {
+            amin = fmin(gth, gph * theta / -gphi);
+            if (theta <= w.cst[DK_THMIN]) amin = fmin(amin, exp(lsw));
+        } else {
+            amin = gth;
+        }
+        amin = uni(amin * gal);
+        // ---- filter line search: trial u = U + a dU, rolled out
+        double a = ap;
+        double la = uni(log(ap));
+        bool accepted = false, ftype = false;
+        double ctr[RPL];
+        double ft = 0.0, lgt = 0.0;
+        while (a >= amin) {
+            RELANE();
+            if (lane < 16) Ut[lane] = fma(a, w.dU[lane], U[lane]);
+            wave_sync();
+            dd_rollout<N>(w.cst, Ut, STt, lane);
+            wave_sync();
+            double tht = 0.0;
+            ft = 0.0;
+            lgt = 0.0;
+            bool bad = false;
+#pragma unroll
+            for (int q = 0; q < RPL; ++q) {
+                double o[6];
+#pragma unroll
+                for (int i = 0; i < 6; ++i) o[i] = w.obs6[6 * roi[q] + i];
+                ctr[q] = dd_row<N, false>(rtype[q], rk[q], o, w.cst, STt, Ut, nullptr, hx);
+                const double st = sr[q] + a * dS[q];
+                if (rtype[q] < D_NONE) tht += fabs(ctr[q] - st);
+                if (rtype[q] == D_OBJ) ft += ctr[q];
+                const double d1 = st - cl[q], d2 = cu[q] - st;
+                if (HL(q) && !(d1 > 0)) bad = true;
+                if (HU(q) && !(d2 > 0)) bad = true;
+                lgt += HL(q) ? (HU(q) ? log(d1 * d2) : log(d1)) : (HU(q) ? log(d2) : 0.0);
+            }
+            wsum2(ft, tht);
+            lgt = wsum(lgt);
+            const bool anybad = __ballot(bad) != 0ull;
+            const double pht = anybad ? INFINITY : ft - mu * lgt;
+            bool ok = isfinite(pht) && tht < w.cst[DK_THMAX];
+            if (ok) {
+                const bool b0 = lane < nf && !(tht < fth0 || pht < fph0);
+                const bool b1 = lane + WAVE < nf && !(tht < fth1 || pht < fph1);
+                ok = __ballot(b0 || b1) == 0ull;
+            }
+            if (ok) {
+                const bool switching = gphi < 0 && la > lsw;
+                if (switching && theta <= w.cst[DK_THMIN]) {
+                    if (pht <= phi + eta * a * gphi) {
+                        accepted = true;
+                        ftype = true;
+                    }
+                } else if (tht <= (1 - gth) * theta || pht <= phi - gph * theta) {
+                    accepted = true;
+                    ftype = false;
+                }
+            }
+            if (accepted) break;
+            a = uni(a * 0.5);
+            la = uni(la - M_LN2);
+        }
+        RELANE();
+        if (accepted) {
+            if (!ftype && nf < FILTER_CAP) {
+                const double fvt = (1 - gth) * theta, fvp = phi - gph * theta;
+                if ((nf & (WAVE - 1)) == lane) {
+                    if (nf < WAVE) {
+                        fth0 = fvt;
+                        fph0 = fvp;
+                    } else {
+                        fth1 = fvt;
+                        fph1 = fvp;
+                    }
+                }
+                nf++;
+            }
+            // the trial point becomes the current one (swap the table roles)
+            double* t1 = ST; ST = STt; STt = t1;
+            double* t2 = U; U = Ut; Ut = t2;
+#pragma unroll
+            for (int q = 0; q < RPL; ++q) {
+                sr[q] += a * dS[q];
+                cr[q] = ctr[q];
+            }
+            f_cur = ft;
+            lsum_cur = lgt;
+        } else {
+            // restoration substitute: shortest tried step, slacks reset onto c(u), filter reset
+            a = uni(fmax(a, amin));
+            if (lane < 16) Ut[lane] = fma(a, w.dU[lane], U[lane]);
+            wave_sync();
+            dd_rollout<N>(w.cst, Ut, STt, lane);
+            wave_sync();
+            double* t1 = ST; ST = STt; STt = t1;
+            double* t2 = U; U = Ut; Ut = t2;
+            double fr = 0.0, lr = 0.0;
+#pragma unroll
+            for (int q = 0; q < RPL; ++q) {
+                double o[6];
+#pragma unroll
+                for (int i = 0; i < 6; ++i) o[i] = w.obs6[6 * roi[q] + i];
+                cr[q] = dd_row<N, false>(rtype[q], rk[q], o, w.cst, ST, U, nullptr, hx);
+                double v = cr[q];
+                const double pl = HL(q) ? fmin(1e-2 * fmax(1.0, fabs(cl[q])), 1e-2 * (cu[q] - cl[q])) : 0.0;
+                const double pu = HU(q) ? fmin(1e-2 * fmax(1.0, fabs(cu[q])), 1e-2 * (cu[q] - cl[q])) : 0.0;
+                if (HL(q) && HU(q))
+                    v = fmin(fmax(v, cl[q] + pl), cu[q] - pu);
+                else if (HL(q))
+                    v = fmax(v, cl[q] + pl);
+                else if (HU(q))
+                    v = fmin(v, cu[q] - pu);
+                sr[q] = rtype[q] < D_NONE ? v : 0.0;
+                const double d1 = sr[q] - cl[q], d2 = cu[q] - sr[q];
+                lr += HL(q) ? (HU(q) ? log(d1 * d2) : log(d1)) : (HU(q) ? log(d2) : 0.0);
+                if (rtype[q] == D_OBJ) fr += cr[q];
+            }
+            wsum2(fr, lr);
+            f_cur = fr;
+            lsum_cur = lr;
+            nf = 0;
+            n_rest++;
+            double viol = 0.0;
+#pragma unroll
+            for (int q = 0; q < RPL; ++q) {
+                const int r = lane + WAVE * q;
+                if (r < mr4 && rtype[q] < D_NONE) {
+                    if (HL(q)) viol = fmax(viol, w.rclo[r] - cr[q]);
+                    if (HU(q)) viol = fmax(viol, cr[q] - w.rcuo[r]);
+                }
+            }
+            viol = wmax(viol);
+            if (n_rest >= REST_FAIL && viol > 1e-4) {
+                status = 2;
+                it++;
+                break;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < RPL; ++q) {
+            zl[q] += az * dZl[q];
+            zu[q] += az * dZu[q];
+            const double d1 = sr[q] - cl[q], d2 = cu[q] - sr[q];
+            idl[q] = HL(q) ? rcp_nr(d1) : 0.0;
+            idu[q] = HU(q) ? rcp_nr(d2) : 0.0;
+            zl[q] = HL(q) ? fmin(fmax(zl[q], mu * 1e-10 * idl[q]), 1e10 * mu * idl[q]) : 0.0;
+            zu[q] = HU(q) ? fmin(fmax(zu[q], mu * 1e-10 * idu[q]), 1e10 * mu * idu[q]) : 0.0;
+        }
+        wave_sync();
+    }
+    // ---- status + outputs (split rows measure the reference's f_en violation exactly)
+    wave_sync();
+    RELANE();
+    if (status != 0 && status != 2) {
+        double viol = 0.0;
+#pragma unroll
+        for (int q = 0; q < RPL; ++q) {
+            const int r = lane + WAVE * q;
+            if (r < mr4 && rtype[q] < D_NONE) {
+                if (HL(q)) viol = fmax(viol, w.rclo[r] - cr[q]);
+                if (HU(q)) viol = fmax(viol, cr[q] - w.rcuo[r]);
+            }
+        }
+        viol = wmax(viol);
+        if (e0 <= w.cst[DK_ACCTOL])
+            status = 1;
+        else if (viol > 1e-4)
+            status = 2;
+    }
+    if (lane < n) P.u_out[(size_t)b * n + lane] = U[lane];
+    if (P.foot_out && lane < 3) P.foot_out[3 * b + lane] = lane < 2 ? U[lane] : 0.0;
+    if (P.x_pred && lane < 3 * N) P.x_pred[(size_t)b * 3 * N + lane] = ST[DD_ST * (lane / 3 + 1) + lane % 3];
+    if (lane == 0) {
+        if (P.status) P.status[b] = status;
+        if (P.iters) P.iters[b] = it;
+    }
+#undef RELANE
+#undef HL
+#undef HU
+}
+
+// DD eval kernel: the reference callbacks (f, grad f, c, J, cl, cu, row activity) at given u, padded
+// layout [circle slots, ellipse slots, f_en] per step
+template <int N>
+__global__ __launch_bounds__(256, 4) void dd_eval_kernel(KP Pv)
+{
+    constexpr int n = 2 * N;
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    KP* Ps = reinterpret_cast<KP*>(smem);
+    double* wsb = smem + KP_DOUBLES;
+    if (threadIdx.x == 0) *Ps = Pv;
+    __syncthreads();
+    const KP& P = *Ps;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
+    const int lane = lane_id();
+    const long long b = (long long)blockIdx.x * WAVES_PER_BLOCK + wv;
+    if (b >= P.B) return;
+    const int mo4 = rfl(P.mo4), m_max = rfl(P.m_max), rps = rfl(P.rps);
+    const int nc_max = rfl(P.nc_max), ne_max = rfl(P.ne_max), nobs = nc_max + ne_max;
+    DDW<N> w = carve_dd<N>(wsb + (size_t)wv * ddw_doubles<N>(nobs, mo4), nobs, mo4);
+    int ncv, nev;
+    dd_prologue<N>(P, w, b, lane, nc_max, ne_max, ncv, nev);
+    dd_rollout<N>(w.cst, w.Ua, w.STa, lane);
+    wave_sync();
+    const size_t mm = (size_t)m_max;
+    double fk = 0.0, hx[8];
+    for (int r = lane; r < m_max + N; r += WAVE) {
+        int t, k, oi;
+        if (r < m_max) {
+            dd_decode(r, rps, m_max, nc_max, ne_max, ncv, nev, false, t, k, oi);
+        } else {
+            t = D_OBJ;
+            k = r - m_max + 1;
+            oi = 0;
+        }
+        double o[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) o[i] = w.obs6[6 * oi + i];
+        // OBJ rows: grad f_k into LDS scratch; constraint rows: J row straight to HBM (or scratch)
+        double* jo = t == D_OBJ ? w.Jd + 16 * (r - m_max)
+                                : (P.J_out ? P.J_out + (b * mm + r) * n : w.Jd + 16 * (N + (lane & 31)));   // junk scratch
+        const double c = dd_row<N, true>(t, k, o, w.cst, w.STa, w.Ua, jo, hx);
+        if (t == D_OBJ) {
+            fk += c;
+        } else {
+            double clv, cuv;
+            dd_bounds(P, t, clv, cuv);
+            if (P.c_out) P.c_out[b * mm + r] = c;
+            if (P.cl_out) P.cl_out[b * mm + r] = clv;
+            if (P.cu_out) P.cu_out[b * mm + r] = cuv;
+            if (P.active_out) P.active_out[b * mm + r] = t != D_NONE;
+        }
+    }
+    const double f = wsum(fk);
+    wave_sync();
+    if (lane < n && P.grad_out) {
+        double g = 0.0;
+        for (int k = 0; k < N; ++k) g += w.Jd[16 * k + lane];
+        P.grad_out[b * n + lane] = g;
+    }
+    if (lane == 0) {
+        if (P.f_out) P.f_out[b] = f;
+        if (P.goal_eff_out) {
+            P.goal_eff_out[2 * b] = P.goal[2 * b];
+            P.goal_eff_out[2 * b + 1] = P.goal[2 * b + 1];
+        }
+    }
+}
+
 }  // namespace alip
 
 // ================================================================================================
@@ -1849,6 +2765,17 @@ void build_tables(const alipmpc_cfg& cfg, int NCPP, int NCPU, std::vector<double
 
 size_t smem_bytes(const Handle* h, bool solve)
 {
+    if (h->cfg.variant == ALIPMPC_VARIANT_DD) {
+        int wsd = 0;
+        switch (h->N) {
+#define DDCASE(NN) \
+    case NN: wsd = ddw_doubles<NN>(h->cfg.nc_max + h->cfg.ne_max, h->mo4); break;
+            DDCASE(1) DDCASE(2) DDCASE(3) DDCASE(4) DDCASE(5) DDCASE(6)
+#undef DDCASE
+        }
+        (void)solve;
+        return sizeof(double) * ((size_t)KP_DOUBLES + (size_t)WAVES_PER_BLOCK * wsd);
+    }
     int wsd = 0;
     switch (h->N) {
 #define WSCASE(NN)                                                                                     \
@@ -1894,6 +2821,8 @@ KP make_kp(const Handle* h, long long B, bool solve)
     P.bvy_hi = c.bvy_hi;
     P.dth = c.dtheta_max;
     P.mu_init = c.mu_init;
+    P.dt = c.dt;
+    P.dd_t = c.dd_t;
     P.G = solve ? h->dGp : h->dGu;
     P.E = solve ? h->dEp : h->dEu;
     P.Gu = h->dGu;
@@ -1942,9 +2871,39 @@ hipError_t launch_t(bool solve, const KP& P, size_t smem, hipStream_t st)
     return hipGetLastError();
 }
 
+template <int N>
+hipError_t launch_dd(bool solve, const KP& P, size_t smem, hipStream_t st)
+{
+    const unsigned grid = (unsigned)((P.B + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
+    auto go = [&](auto kern) {
+        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(WAVE * WAVES_PER_BLOCK), smem, st, P);
+    };
+    if (!solve)
+        go(dd_eval_kernel<N>);
+    else if (P.mo4 <= WAVE)
+        go(dd_solve_kernel<N, 1>);
+    else if (P.mo4 <= 2 * WAVE)
+        go(dd_solve_kernel<N, 2>);
+    else
+        go(dd_solve_kernel<N, 3>);
+    return hipGetLastError();
+}
+
 hipError_t launch(const Handle* h, bool solve, const KP& P, hipStream_t st)
 {
     const size_t smem = smem_bytes(h, solve);
+    if (h->cfg.variant == ALIPMPC_VARIANT_DD) {
+        switch (h->N) {
+        case 1: return launch_dd<1>(solve, P, smem, st);
+        case 2: return launch_dd<2>(solve, P, smem, st);
+        case 3: return launch_dd<3>(solve, P, smem, st);
+        case 4: return launch_dd<4>(solve, P, smem, st);
+        case 5: return launch_dd<5>(solve, P, smem, st);
+        case 6: return launch_dd<6>(solve, P, smem, st);
+        }
+        return hipErrorInvalidValue;
+    }
     switch (h->N) {
     case 1: return launch_t<1>(solve, P, smem, st);
     case 2: return launch_t<2>(solve, P, smem, st);
@@ -2052,8 +3011,10 @@ int alipmpc_create(const alipmpc_cfg* cfg, int device, void** handle)
     if (cfg->N < 1 || cfg->N > ALIPMPC_MAX_N || cfg->nc_max < 0 || cfg->ne_max < 0 ||
         cfg->nc_max + cfg->ne_max > ALIPMPC_MAX_OBS || cfg->max_iter < 0 || cfg->max_iter > FILTER_CAP - 2)
         return ALIPMPC_EINVAL;
-    if (cfg->variant == ALIPMPC_VARIANT_DD || cfg->precision != ALIPMPC_PREC_FP64) return ALIPMPC_EUNSUPPORTED;
-    if (cfg->variant != ALIPMPC_VARIANT_MODI && cfg->variant != ALIPMPC_VARIANT_SIG_STEP) return ALIPMPC_EINVAL;
+    if (cfg->precision != ALIPMPC_PREC_FP64) return ALIPMPC_EUNSUPPORTED;
+    if (cfg->variant != ALIPMPC_VARIANT_MODI && cfg->variant != ALIPMPC_VARIANT_SIG_STEP &&
+        cfg->variant != ALIPMPC_VARIANT_DD)
+        return ALIPMPC_EINVAL;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return ALIPMPC_ENODEV;
     hipDeviceProp_t prop;
@@ -2070,11 +3031,21 @@ int alipmpc_create(const alipmpc_cfg* cfg, int device, void** handle)
     h->rps = alipmpc_rows_per_step(cfg);
     h->m_max = cfg->N * h->rps;
     h->mr4 = (h->m_max + 3) & ~3;
-    h->rps_s = h->rps + (cfg->variant == ALIPMPC_VARIANT_MODI ? 1 : 0);   // f_en -> two smooth rows
-    h->m_s = cfg->N * h->rps_s;
-    h->mr4_s = (h->m_s + 3) & ~3;
-    // + the objective pseudo-rows of the solve kernel, rounded up to the compiled J-layout size (4 KSM)
-    h->mo4 = 4 * ksm_of(h->mr4_s + 4 * ((cfg->N + 3) / 4));
+    if (cfg->variant == ALIPMPC_VARIANT_DD) {
+        // DD solve rows per step: cbf slots, v +- s w, v bound, w bound; + N objective rows; whole
+        // 64-lane row groups (dd_solve_kernel<N, RPL>)
+        h->rps_s = cfg->nc_max + cfg->ne_max + 4;
+        h->m_s = cfg->N * h->rps_s;
+        h->mr4_s = (h->m_s + 3) & ~3;
+        const int rpl = (h->mr4_s + cfg->N + WAVE - 1) / WAVE;
+        h->mo4 = rpl <= 3 ? WAVE * rpl : 1 << 20;
+    } else {
+        h->rps_s = h->rps + (cfg->variant == ALIPMPC_VARIANT_MODI ? 1 : 0);   // f_en -> two smooth rows
+        h->m_s = cfg->N * h->rps_s;
+        h->mr4_s = (h->m_s + 3) & ~3;
+        // + the objective pseudo-rows of the solve kernel, rounded up to the compiled J-layout size (4 KSM)
+        h->mo4 = 4 * ksm_of(h->mr4_s + 4 * ((cfg->N + 3) / 4));
+    }
     if (h->mr4 > MAX_ROWS || h->mo4 > MAX_ROWS + 64) {
         delete h;
         return ALIPMPC_EINVAL;
@@ -2105,24 +3076,27 @@ int alipmpc_create(const alipmpc_cfg* cfg, int device, void** handle)
 
 static int run_batch(Handle* h, bool solve, int64_t B, const double* x0, const double* goal, const int8_t* leg,
                      const double* cir, const int32_t* nc, const double* elp, const int32_t* ne, const double* u0,
-                     double* u_out, double* foot_out, double* x_pred, int32_t* status, int32_t* iters, double* f,
+                     const double* last_u, double* u_out, double* foot_out, double* x_pred, int32_t* status, int32_t* iters, double* f,
                      double* grad, double* c, double* J, double* cl, double* cu, double* goal_eff, int8_t* row_active,
                      void* hip_stream)
 {
     if (!h) return ALIPMPC_EINVAL;
     if (B < 0) return fail(h, ALIPMPC_EINVAL, "B < 0");
     if (B == 0) return ALIPMPC_OK;
-    if (!x0 || !goal || !leg || !nc || !u0 || (h->cfg.nc_max > 0 && !cir) || (h->cfg.ne_max > 0 && (!elp || !ne)))
+    const alipmpc_cfg& cf = h->cfg;
+    const bool dd = cf.variant == ALIPMPC_VARIANT_DD;
+    if (!x0 || !goal || (!leg && !dd) || !nc || !u0 || (cf.nc_max > 0 && !cir) || (cf.ne_max > 0 && (!elp || !ne)))
         return fail(h, ALIPMPC_EINVAL, "missing input pointer");
     if (solve && !u_out) return fail(h, ALIPMPC_EINVAL, "u_out is required");
     HIPCHK(h, hipSetDevice(h->device));
-    const alipmpc_cfg& cf = h->cfg;
-    const int n = 5 * h->N, N = h->N;     // host-facing u is the reference's 5N-vector
+    // host-facing u: the reference's 5N-vector (LIP) / 2N controls (DD); state dimension 5 / 3
+    const int N = h->N, n = dd ? 2 * N : 5 * N, sd = dd ? 3 : 5;
     const size_t mm_ = (size_t)h->m_max;
     KP P = make_kp(h, B, solve);
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : h->own;
     if (hip_stream) {
         P.x0 = x0; P.goal = goal; P.leg = leg; P.cir = cir; P.nc = nc; P.elp = elp; P.ne = ne; P.u0 = u0;
+        P.last_u = last_u;
         P.u_out = u_out; P.foot_out = foot_out; P.x_pred = x_pred; P.status = status; P.iters = iters;
         P.f_out = f; P.grad_out = grad; P.c_out = c; P.J_out = J; P.cl_out = cl; P.cu_out = cu;
         P.goal_eff_out = goal_eff; P.active_out = row_active;
@@ -2137,9 +3111,10 @@ static int run_batch(Handle* h, bool solve, int64_t B, const double* x0, const d
     size_t need = 0;
     {
         Carver cv{nullptr};
-        cv.take<double>(Bz * 5); cv.take<double>(Bz * 2); cv.take<int8_t>(Bz); cv.take<double>(Bz * 3 * cf.nc_max);
+        cv.take<double>(Bz * sd); cv.take<double>(Bz * 2); cv.take<int8_t>(Bz); cv.take<double>(Bz * 3 * cf.nc_max);
         cv.take<int32_t>(Bz); cv.take<double>(Bz * 5 * cf.ne_max); cv.take<int32_t>(Bz); cv.take<double>(Bz * n);
-        cv.take<double>(Bz * n); cv.take<double>(Bz * 3); cv.take<double>(Bz * 5 * N); cv.take<int32_t>(Bz);
+        cv.take<double>(Bz * 2);
+        cv.take<double>(Bz * n); cv.take<double>(Bz * 3); cv.take<double>(Bz * sd * N); cv.take<int32_t>(Bz);
         cv.take<int32_t>(Bz); cv.take<double>(Bz); cv.take<double>(Bz * n); cv.take<double>(Bz * mm_);
         cv.take<double>(Bz * mm_ * n); cv.take<double>(Bz * mm_); cv.take<double>(Bz * mm_); cv.take<double>(Bz * 2);
         cv.take<int8_t>(Bz * mm_);
@@ -2147,7 +3122,7 @@ static int run_batch(Handle* h, bool solve, int64_t B, const double* x0, const d
     }
     if (int e = ensure_stage(h, need)) return e;
     Carver cv{(char*)h->stage};
-    double* d_x0 = cv.take<double>(Bz * 5);
+    double* d_x0 = cv.take<double>(Bz * sd);
     double* d_goal = cv.take<double>(Bz * 2);
     int8_t* d_leg = cv.take<int8_t>(Bz);
     double* d_cir = cv.take<double>(Bz * 3 * cf.nc_max);
@@ -2155,9 +3130,10 @@ static int run_batch(Handle* h, bool solve, int64_t B, const double* x0, const d
     double* d_elp = cv.take<double>(Bz * 5 * cf.ne_max);
     int32_t* d_ne = cv.take<int32_t>(Bz);
     double* d_u0 = cv.take<double>(Bz * n);
+    double* d_lu = cv.take<double>(Bz * 2);
     double* d_u = cv.take<double>(Bz * n);
     double* d_foot = cv.take<double>(Bz * 3);
-    double* d_xp = cv.take<double>(Bz * 5 * N);
+    double* d_xp = cv.take<double>(Bz * sd * N);
     int32_t* d_st = cv.take<int32_t>(Bz);
     int32_t* d_it = cv.take<int32_t>(Bz);
     double* d_f = cv.take<double>(Bz);
@@ -2170,9 +3146,9 @@ static int run_batch(Handle* h, bool solve, int64_t B, const double* x0, const d
     int8_t* d_ra = cv.take<int8_t>(Bz * mm_);
     auto h2d = [&](void* d, const void* s, size_t bytes) { return hipMemcpyAsync(d, s, bytes, hipMemcpyHostToDevice, st); };
     auto d2h = [&](void* d, const void* s, size_t bytes) { return hipMemcpyAsync(d, s, bytes, hipMemcpyDeviceToHost, st); };
-    HIPCHK(h, h2d(d_x0, x0, Bz * 5 * 8));
+    HIPCHK(h, h2d(d_x0, x0, Bz * sd * 8));
     HIPCHK(h, h2d(d_goal, goal, Bz * 2 * 8));
-    HIPCHK(h, h2d(d_leg, leg, Bz));
+    if (leg) HIPCHK(h, h2d(d_leg, leg, Bz));
     if (cf.nc_max) HIPCHK(h, h2d(d_cir, cir, Bz * 3 * cf.nc_max * 8));
     HIPCHK(h, h2d(d_nc, nc, Bz * 4));
     if (cf.ne_max) {
@@ -2180,7 +3156,9 @@ static int run_batch(Handle* h, bool solve, int64_t B, const double* x0, const d
         HIPCHK(h, h2d(d_ne, ne, Bz * 4));
     }
     HIPCHK(h, h2d(d_u0, u0, Bz * n * 8));
-    P.x0 = d_x0; P.goal = d_goal; P.leg = d_leg; P.cir = d_cir; P.nc = d_nc;
+    if (last_u) HIPCHK(h, h2d(d_lu, last_u, Bz * 2 * 8));
+    P.last_u = last_u ? d_lu : nullptr;
+    P.x0 = d_x0; P.goal = d_goal; P.leg = leg ? d_leg : nullptr; P.cir = d_cir; P.nc = d_nc;
     P.elp = cf.ne_max ? d_elp : nullptr; P.ne = cf.ne_max ? d_ne : nullptr; P.u0 = d_u0;
     if (solve) {
         P.u_out = d_u; P.foot_out = d_foot; P.x_pred = d_xp; P.status = d_st; P.iters = d_it;
@@ -2195,7 +3173,7 @@ static int run_batch(Handle* h, bool solve, int64_t B, const double* x0, const d
     if (solve) {
         HIPCHK(h, d2h(u_out, d_u, Bz * n * 8));
         if (foot_out) HIPCHK(h, d2h(foot_out, d_foot, Bz * 3 * 8));
-        if (x_pred) HIPCHK(h, d2h(x_pred, d_xp, Bz * 5 * N * 8));
+        if (x_pred) HIPCHK(h, d2h(x_pred, d_xp, Bz * sd * N * 8));
         if (status) HIPCHK(h, d2h(status, d_st, Bz * 4));
         if (iters) HIPCHK(h, d2h(iters, d_it, Bz * 4));
     } else {
@@ -2217,8 +3195,7 @@ int alipmpc_solve_batch(void* handle, int64_t B, const double* x0, const double*
                         const double* last_u, double* u_out, double* foot_out, double* x_pred, int32_t* status,
                         int32_t* iters, void* hip_stream)
 {
-    (void)last_u;
-    return run_batch((Handle*)handle, true, B, x0, goal, leg, cir, nc, elp, ne, u0, u_out, foot_out, x_pred, status,
+    return run_batch((Handle*)handle, true, B, x0, goal, leg, cir, nc, elp, ne, u0, last_u, u_out, foot_out, x_pred, status,
                      iters, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, hip_stream);
 }
 
@@ -2227,8 +3204,7 @@ int alipmpc_eval_batch(void* handle, int64_t B, const double* x0, const double* 
                        const double* last_u, double* f, double* grad, double* c, double* J, double* cl, double* cu,
                        double* goal_eff, int8_t* row_active, void* hip_stream)
 {
-    (void)last_u;
-    return run_batch((Handle*)handle, false, B, x0, goal, leg, cir, nc, elp, ne, u, nullptr, nullptr, nullptr,
+    return run_batch((Handle*)handle, false, B, x0, goal, leg, cir, nc, elp, ne, u, last_u, nullptr, nullptr, nullptr,
                      nullptr, nullptr, f, grad, c, J, cl, cu, goal_eff, row_active, hip_stream);
 }
 

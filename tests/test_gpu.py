@@ -229,3 +229,58 @@ def test_full_size_properties_cfg3(gpu_lib):
     A, Bm = pl._alip_matrices(beta, 0.4, 0.4)
     x1 = bt["x0"] @ A.T + o["foot"] @ Bm.T
     assert np.max(np.abs(x1 - o["x_pred"][:, 0])) < 1e-12
+
+
+# ---------------------------------------------------------------- DD variant (MPC_DD_sig_step.py)
+def _dd_batch(B, seed, n_cir=5, N=3):
+    from alipmpc import scenes
+    bt = scenes.make_batch(B, seed=seed, n_cir=n_cir, N=N)
+    rng = np.random.default_rng(seed + 17)
+    x0 = np.stack([bt["x0"][:, 0], bt["x0"][:, 1], bt["x0"][:, 4]], 1)
+    last_u = np.stack([rng.uniform(0.45, 0.75, B), rng.uniform(-0.15, 0.15, B)], 1)
+    return dict(x0=x0, goal=bt["goal"], cir=bt["cir"], nc=bt["nc"], last_u=last_u, u0=np.tile(last_u, (1, N)))
+
+
+def test_dd_eval_matches_reference_callbacks(gpu_lib, golden):
+    g = golden("g1_callbacks_dd")
+    s = gpu_lib.Solver(gpu_lib.default_cfg(2))
+    o = s.eval(g["x0"], g["goal"], None, g["cir"], g["nc"], g["elp"], g["ne"], g["u"], last_u=g["last_u"])
+    assert rel(o["f"], g["f"]) < REL
+    assert rel(o["grad"], g["grad"]) < REL
+    for t in range(len(g["f"])):
+        act = o["row_active"][t].astype(bool)
+        assert act.sum() == g["m"][t]
+        assert rel(o["c"][t][act], g["c"][t][:g["m"][t]]) < REL
+        assert rel(o["J"][t][act], g["J"][t][:g["m"][t]]) < REL
+
+
+def test_dd_solve_matches_scipy_goldens(gpu_lib, golden, coracle):
+    d = golden("g3_synthetic_dd")
+    good = (d["agree"] < 1e-6) & (d["viol"] < 1e-8)
+    s = gpu_lib.Solver(gpu_lib.default_cfg(2, nc_max=6, ne_max=6, max_iter=100))   # to convergence
+    o = s.solve(d["x0"], d["goal"], None, d["cir"], d["nc"], d["elp"], d["ne"], u0=d["u0"], last_u=d["last_u"])
+    err = np.max(np.abs(o["u"] - d["u_ref"]), axis=1)
+    assert np.all(err[good] < 1e-4), err[good].max()
+    cc = coracle.default_cfg(2, nc_max=6, ne_max=6, max_iter=100)
+    r = coracle.solve_batch_dd(cc, d["x0"], d["goal"], d["cir"], d["nc"], d["elp"], d["ne"], d["u0"], d["last_u"])
+    assert (o["status"] == r["status"]).mean() >= 0.95
+    both = (o["status"] == 0) & (r["status"] == 0)
+    assert (np.max(np.abs(o["u"] - r["u"]), axis=1)[both] < 1e-6).mean() >= 0.95
+    assert np.allclose(o["foot"][:, :2], o["u"][:, :2]) and np.all(o["foot"][:, 2] == 0)
+
+
+@pytest.mark.parametrize("N", [3, 5])
+def test_dd_batch_vs_oracle(gpu_lib, coracle, N):
+    bt = _dd_batch(512, seed=40 + N, N=N)
+    s = gpu_lib.Solver(gpu_lib.default_cfg(2, N, nc_max=5, ne_max=0))
+    o = s.solve(bt["x0"], bt["goal"], None, bt["cir"], bt["nc"], u0=bt["u0"], last_u=bt["last_u"])
+    cc = coracle.default_cfg(2, N, nc_max=5, ne_max=0)
+    r = coracle.solve_batch_dd(cc, bt["x0"], bt["goal"], bt["cir"], bt["nc"], None, None, bt["u0"], bt["last_u"],
+                               nthreads=8)
+    assert (o["status"] == r["status"]).mean() >= 0.95
+    both = (o["status"] == 0) & (r["status"] == 0)
+    assert both.mean() >= 0.5
+    ok = np.max(np.abs(o["u"] - r["u"]), axis=1) < 1e-4
+    assert ok[both].mean() >= 0.97
+    okx = np.max(np.abs(o["x_pred"] - r["x_pred"]).reshape(len(ok), -1), axis=1) < 1e-4
+    assert okx[both].mean() >= 0.97
