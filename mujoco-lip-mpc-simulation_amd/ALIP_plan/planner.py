@@ -4,6 +4,6 @@ The reference's ALIP_plan/planner.py (class ALIP, planner.py:14) is a legacy one
 nothing imports; the working planner surface callers use is MPCCBF (MPC_LIP_modi.py:13-391), so this
 module exports that surface backed by libalipmpc.so (see alipmpc/planner.py for the signatures).
 """
-from alipmpc.planner import MPCCBF, MPCCBFSigStep  # noqa: F401
+from alipmpc.planner import MPCCBF, MPCCBFDD, MPCCBFSigStep  # noqa: F401
 
-__all__ = ["MPCCBF", "MPCCBFSigStep"]
+__all__ = ["MPCCBF", "MPCCBFSigStep", "MPCCBFDD"]

@@ -11,6 +11,8 @@ Reference surface reproduced (file:line):
   .select_obs(xk) (sets sel_cir / sel_elp) / .xk_track_det / .solve_footdisp / .tube_func
   sig_step: MPCCBFSigStep(goals, obs_param, obs_cbf, margin, step=3); gen_control_test returns the
   4-tuple (xk_list[1:], p_list[0], hd_list, close_2_goal) and solveMPCCBF returns u   MPC_LIP_sig_step.py:14-278
+  DD: MPCCBFDD(goals, cir_param, cir_cbf, elp_param, elp_cbf, margin, step=3); gen_dd_control(state,
+  init_guess, last_u) -> (states, heading, control, close2goal, fesi)                  MPC_DD_sig_step.py:11-193
 Errors: invalid arguments raise ValueError; a solver failure is NOT an exception (feasi = 2, iterate
 returned), exactly like the reference.  Instances are stateful (sel_cir, init_state) and not re-entrant.
 New: solve_batch(states, leg_inds, init_guesses, ...) solves many instances in one kernel launch.
@@ -237,3 +239,77 @@ class MPCCBFSigStep(_Base):
             if d <= 0.35:
                 close_2_goal = True
         return xk_list[1:], p_list[0], hd_list, close_2_goal
+
+
+class MPCCBFDD(_Base):
+    """Drop-in for MPC_DD_sig_step.MPCCBF (unicycle MPC-CBF, MPC_DD_sig_step.py:11-316): state [px, py, th],
+    decision [v, w] x N with v in [0.4, 0.8], |w| <= pi/16, f_en = s|w| + v, smoothness to last_u.
+      gen_dd_control(state, init_guess, last_u, plot=False, trajec=[])
+          -> (states, heading, control, close2goal, fesi)                          :70-121
+      solveMPCCBF(xk, init_guess, last_u) -> (u, fesi)                            :123-193
+    All obstacles are used (select_obs is commented out, :75) and there is no detour goal."""
+    variant = _lib.VARIANT_DD
+
+    def __init__(self, goals, cir_param, cir_cbf, elp_param, elp_cbf, margin, step=3, device=0, **cfg_overrides):
+        self.cir_list = cir_param
+        self.elp_list = elp_param
+        self.cir_safe = np.asarray(cir_cbf, float).reshape(-1, 3)
+        self.elp_safe = np.asarray(elp_cbf, float).reshape(-1, 5)
+        self._setup(goals, margin, step, device, cfg_overrides, len(self.cir_safe), len(self.elp_safe))
+        self.v_max, self.v_min = self.cfg.bvx_hi, self.cfg.bvx_lo
+        self.tot_time = 80
+
+    def tube_func(self, heading_list, init_tube_value):
+        """MPC_DD_sig_step.py:298-316 (its own thresholds: +-0.2, gains 0.3 / 0.7)."""
+        new_heading = np.zeros_like(heading_list, dtype=float)
+        tube = init_tube_value
+        for i, h in enumerate(heading_list):
+            d = h - tube
+            if d > 0:
+                tube += (0.3 if 0.2 > d else 0.7) * d
+            elif d < 0:
+                tube += (0.3 if -0.2 < d else 0.7) * d
+            new_heading[i] = tube
+        return new_heading
+
+    def solveMPCCBF(self, xk, init_guess, last_u):
+        u0 = np.ravel(np.asarray(init_guess, float))
+        if u0.size != 2 * self.N:
+            raise ValueError(f"init_guess must have {2 * self.N} entries")
+        cir, nc = self._padded_cir(1)
+        elp, ne = self._padded_elp(1) if self.cfg.ne_max > 0 else (None, None)
+        out = self.solver.solve(np.ravel(xk)[None], np.ravel(self.goal)[None], None, cir, nc, elp, ne,
+                                u0=u0[None], last_u=np.ravel(np.asarray(last_u, float))[None])
+        self.last_status = int(out["status"][0])
+        self.last_iters = int(out["iters"][0])
+        return out["u"][0], self.last_status
+
+    def gen_dd_control(self, state, init_guess, last_u, plot=False, trajec=[]):
+        self.init_state = np.asarray(state, float).reshape(3, 1)
+        xk = np.ravel(state).astype(float)
+        u, fesi = self.solveMPCCBF(xk, init_guess, last_u)
+        states, heading, control = [list(xk)], [], []
+        g = np.ravel(self.goal)
+        dis2goal = None
+        for i in range(self.N):
+            uk = np.array([u[2 * i:2 * i + 2]]).T
+            xk = xk + np.array([self.dt * math.cos(xk[2]) * uk[0, 0], self.dt * math.sin(xk[2]) * uk[0, 0], uk[1, 0]])
+            if i == 0:
+                dis2goal = math.sqrt(float((xk[0:2] - g) @ (xk[0:2] - g)))
+            states.append(list(xk))
+            heading.append(float(xk[2]))
+            control.append(uk)
+        return states, heading, control, dis2goal <= 0.35, fesi
+
+    def solve_batch(self, states, init_guesses, last_us, goals=None, cir=None, nc=None, elp=None, ne=None):
+        """Many DD instances in one launch: states (B,3), init_guesses (B,2N), last_us (B,2)."""
+        states = np.asarray(states, float).reshape(-1, 3)
+        Bn = len(states)
+        goals = np.tile(np.ravel(self.goal), (Bn, 1)) if goals is None else goals
+        if cir is None:
+            cir, nc = self._padded_cir(Bn)
+        if elp is None and self.cfg.ne_max > 0:
+            elp, ne = self._padded_elp(Bn)
+        return self.solver.solve(states, goals, None, cir, nc, elp, ne,
+                                 u0=np.asarray(init_guesses, float).reshape(Bn, -1),
+                                 last_u=np.asarray(last_us, float).reshape(Bn, 2))

@@ -284,3 +284,30 @@ def test_dd_batch_vs_oracle(gpu_lib, coracle, N):
     assert ok[both].mean() >= 0.97
     okx = np.max(np.abs(o["x_pred"] - r["x_pred"]).reshape(len(ok), -1), axis=1) < 1e-4
     assert okx[both].mean() >= 0.97
+
+
+def test_planner_dropins_match_batched_solver(gpu_lib, golden):
+    """ALIP_plan/planner.py drop-ins (MPCCBF / MPCCBFSigStep / MPCCBFDD) return the reference tuples and the
+    same solution as one batched launch."""
+    import alipmpc.planner as pl
+    d = golden("g3_sup_learn")
+    cir = d["cir_safe"]
+    mp = pl.MPCCBF([[10, 10]], cir, cir, [], [], [-0.5, 10.5])
+    idx = [0, 7, 33]
+    batch = mp.solve_batch(d["x_nex"][idx], d["leg"][idx], d["u0"][idx])
+    for j, i in enumerate(idx):
+        xs, p0, hd, c2g, feasi, pos_det = mp.gen_control_test(d["x_nex"][i], d["leg"][i], d["u0"][i])
+        assert feasi == batch["status"][j]
+        assert np.max(np.abs(p0 - batch["foot"][j])) < 1e-12
+        assert len(xs) == 3 and len(hd) == 3 and pos_det.shape[1] == 2
+        assert np.max(np.abs(np.array(xs) - batch["x_pred"][j])) < 1e-12
+    ss = pl.MPCCBFSigStep([[10, 10]], cir, cir, [-0.5, 10.5])
+    out = ss.gen_control_test(d["x_nex"][0], d["leg"][0], None)
+    assert len(out) == 4 and out[1].shape == (3,)
+    bt = _dd_batch(4, seed=5)
+    dd = pl.MPCCBFDD([[10, 10]], bt["cir"][0][:bt["nc"][0]], bt["cir"][0][:bt["nc"][0]], [], [], [-0.5, 10.5])
+    db = dd.solve_batch(bt["x0"][:1], bt["u0"][:1], bt["last_u"][:1])
+    states, heading, control, c2g, fesi = dd.gen_dd_control(bt["x0"][0], bt["u0"][0], bt["last_u"][0])
+    assert fesi == db["status"][0] and len(states) == 4 and len(control) == 3
+    assert np.max(np.abs(np.array(states[1:]) - db["x_pred"][0])) < 1e-12
+    assert np.max(np.abs(np.ravel(control) - db["u"][0])) < 1e-15
