@@ -8,7 +8,7 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 TAG=${1:-r1}
 step() { echo "=== $*" ; }
-step pytest && timeout -k 10 900 python -m pytest $R/tests -x -q -m gpu > $OUT/pytest_gpu_$TAG.log 2>&1; rc=$?; tail -5 $OUT/pytest_gpu_$TAG.log; [ $rc -eq 0 ] || exit $rc
+step pytest && timeout -k 10 900 python -u -m pytest $R/tests -x -v --timeout 120 --timeout-method thread -m gpu > $OUT/pytest_gpu_$TAG.log 2>&1; rc=$?; tail -5 $OUT/pytest_gpu_$TAG.log; [ $rc -eq 0 ] || exit $rc
 step smoke && timeout -k 10 300 python -c "import sys; sys.path.insert(0,'$R'); import __graft_entry__ as g; g.smoke()" > $OUT/smoke_$TAG.log 2>&1 || { cat $OUT/smoke_$TAG.log; exit 1; }
 cat $OUT/smoke_$TAG.log
 step bench && timeout -k 10 300 python $R/bench.py > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err || { tail -20 $OUT/bench_$TAG.err; exit 1; }
