@@ -237,15 +237,16 @@ def jacobian_sweep(alipmpc, scenes, cfg, args, dev, reps=10):
     st = torch.cuda.current_stream(dev)
     for _ in range(2):
         s.eval_device(inp, out, stream=st)
-    ts = []
-    for _ in range(reps):
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    # back-to-back launches (no host sync in between) so the launch latency overlaps the previous kernel;
+    # per-launch HIP events on the launch stream
+    torch.cuda.synchronize(dev)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for a, b in evs:
         a.record(st)
         s.eval_device(inp, out, stream=st)
         b.record(st)
-        torch.cuda.synchronize(dev)
-        ts.append(a.elapsed_time(b))
-    ms = float(np.mean(ts))
+    torch.cuda.synchronize(dev)
+    ms = float(np.mean([a.elapsed_time(b) for a, b in evs[1:]]))
     per = 8 * (n + 8 + 3 * cfg.nc_max) + 8 * (1 + n + m + m * n)
     gbs = Bs * per / (ms * 1e-3) / 1e9
     return {"kernel": f"eval_kernel<{cfg.N}>", "bound": "hbm", "batch": Bs, "bytes_per_instance": per,

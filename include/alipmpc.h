@@ -22,7 +22,8 @@
  *     stages them through its own device workspace and synchronises before returning.
  *     hip_stream != NULL: all pointers are DEVICE pointers (hipMalloc / torch CUDA tensors) and the call
  *     is asynchronous on that stream (no host synchronisation, no allocation after the first call of a
- *     given batch size — graph-capturable).
+ *     given batch size — graph-capturable).  ALIPMPC_STREAM_NULL selects device pointers on the null
+ *     (default) stream, whose handle value is 0.
  *   - Row-major, instance-major arrays ("B x k" = k contiguous values per instance).
  *   - Return 0 on success, a negative ALIPMPC_E* code on error; alipmpc_last_error(h) gives the text.
  *   - There is no CPU execution path: a handle needs a visible gfx950 device.
@@ -61,6 +62,8 @@ extern "C" {
 #define ALIPMPC_SOLVED_TO_ACCEPTABLE_LEVEL 1
 #define ALIPMPC_INFEASIBLE_PROBLEM_DETECTED 2
 #define ALIPMPC_MAXIMUM_ITERATIONS_EXCEEDED (-1)
+/* rollout only: the instance had already reached its goal, no solve was run at this step */
+#define ALIPMPC_ROLLOUT_DONE (-10)
 
 /* error codes */
 #define ALIPMPC_OK 0
@@ -68,6 +71,9 @@ extern "C" {
 #define ALIPMPC_ENODEV (-2)
 #define ALIPMPC_EHIP (-3)
 #define ALIPMPC_EUNSUPPORTED (-4)
+
+/* hip_stream value meaning "device pointers, asynchronous on the null (default) stream" */
+#define ALIPMPC_STREAM_NULL ((void*)(intptr_t)-1)
 
 #define ALIPMPC_MAX_N 6      /* horizon limit of the kernels (n = 5N <= 32 -> two 16-column MFMA tiles) */
 #define ALIPMPC_MAX_OBS 24   /* nc_max + ne_max limit (and N * rows_per_step <= 128) */
@@ -144,6 +150,32 @@ int alipmpc_eval_batch(void* handle, int64_t B,
                        double* f, double* grad, double* c, double* J,
                        double* cl, double* cu, double* goal_eff, int8_t* row_active,
                        void* hip_stream);
+
+/*
+ * Closed-loop receding-horizon rollout of B independent episodes for up to S steps on an ideal ALIP plant
+ * (the batch harness that replaces the data_log replay loop: main_sim_mpc.py:66-131 driving
+ * logger_mpc.py:318-341 gen_nex_foot_input -> MPCCBF.gen_control_test).  Step t: solve every active
+ * instance (as alipmpc_solve_batch), execute the first planned step (x <- x_pred[0], the state at the next
+ * touchdown = get_next_states over a full step), switch stance (leg <- -leg), warm-start the next solve
+ * from the plan (modi: previous x_mpc_tar unshifted, logger_mpc.py:325-331; sig_step: [g2..gN, gN],
+ * MPC_LIP_sig_step.py:186-189; DD: previous controls and last_u <- first control), and retire the
+ * instance once close_2_goal holds (the episode stops after that step, main_sim_mpc.py:121-131).
+ * Inputs as alipmpc_solve_batch (x0/leg/u0/last_u = the first step's).  Outputs (any may be NULL):
+ *   foot_traj     B x S x 3        p_list[0] of each step (NaN after the goal)
+ *   x_traj        B x (S+1) x sdim touchdown states x^(0) = x0, x^(1), ...
+ *   status_traj   B x S            solve status per step (ALIPMPC_ROLLOUT_DONE after the goal)
+ *   iters_traj    B x S            interior-point iterations per step
+ *   steps_to_goal B                steps taken until close_2_goal (-1: not within S)
+ * Host pointers when hip_stream == NULL, else device pointers (asynchronous; S solve launches + S small
+ * plant-update launches on the stream, no host synchronisation).
+ */
+int alipmpc_rollout_batch(void* handle, int64_t B, int32_t S,
+                          const double* x0, const double* goal, const int8_t* leg,
+                          const double* cir, const int32_t* nc,
+                          const double* elp, const int32_t* ne,
+                          const double* u0, const double* last_u,
+                          double* foot_traj, double* x_traj, int32_t* status_traj, int32_t* iters_traj,
+                          int32_t* steps_to_goal, void* hip_stream);
 
 /* Duration in milliseconds of the most recent solve kernel launch on this handle, measured with HIP
  * events on the launch stream (0 if none). */

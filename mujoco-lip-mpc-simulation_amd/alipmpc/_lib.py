@@ -16,7 +16,8 @@ VARIANT_MODI, VARIANT_SIG_STEP, VARIANT_DD = 0, 1, 2
 PREC_FP64, PREC_FP32 = 0, 1
 
 STATUS_NAMES = {0: "Solve_Succeeded", 1: "Solved_To_Acceptable_Level", 2: "Infeasible_Problem_Detected",
-                -1: "Maximum_Iterations_Exceeded"}
+                -1: "Maximum_Iterations_Exceeded", -10: "Rollout_Done (goal reached earlier, not solved)"}
+ROLLOUT_DONE = -10
 
 _ERRORS = {-1: "EINVAL", -2: "ENODEV (no visible gfx950 device)", -3: "EHIP", -4: "EUNSUPPORTED"}
 
@@ -34,7 +35,7 @@ class Cfg(ctypes.Structure):
 
 
 EXPORTS = ("alipmpc_default_cfg", "alipmpc_rows_per_step", "alipmpc_num_vars", "alipmpc_create",
-           "alipmpc_solve_batch", "alipmpc_eval_batch", "alipmpc_last_kernel_ms", "alipmpc_last_error",
+           "alipmpc_solve_batch", "alipmpc_eval_batch", "alipmpc_rollout_batch", "alipmpc_last_kernel_ms", "alipmpc_last_error",
            "alipmpc_destroy")
 
 _lib = None
@@ -70,6 +71,8 @@ def load(build_if_missing=True):
     L.alipmpc_solve_batch.restype = ctypes.c_int
     L.alipmpc_eval_batch.argtypes = [P, ctypes.c_int64] + [P] * 18
     L.alipmpc_eval_batch.restype = ctypes.c_int
+    L.alipmpc_rollout_batch.argtypes = [P, ctypes.c_int64, ctypes.c_int32] + [P] * 15
+    L.alipmpc_rollout_batch.restype = ctypes.c_int
     L.alipmpc_last_kernel_ms.argtypes = [P]
     L.alipmpc_last_kernel_ms.restype = ctypes.c_double
     L.alipmpc_last_error.argtypes = [P]
@@ -98,6 +101,16 @@ def rows_per_step(cfg):
 
 def num_vars(cfg):
     return int(load().alipmpc_num_vars(ctypes.byref(cfg)))
+
+
+STREAM_NULL = ctypes.c_void_p(ctypes.c_size_t(-1).value)   # ALIPMPC_STREAM_NULL
+
+
+def _stream_arg(st):
+    """Device-pointer mode needs a non-NULL stream argument: torch's default stream has handle 0, which the
+    ABI reads as host-pointer mode, so it is passed as ALIPMPC_STREAM_NULL."""
+    h = int(st.cuda_stream)
+    return ctypes.c_void_p(h) if h else STREAM_NULL
 
 
 def _ptr(a):
@@ -189,7 +202,36 @@ class Solver:
         self._check(rc, "alipmpc_eval_batch")
         return out
 
+    def rollout(self, x0, goal, leg, cir, nc, elp=None, ne=None, u0=None, last_u=None, steps=8):
+        """Closed-loop receding-horizon rollout (alipmpc_rollout_batch) from host arrays.  Returns
+        dict(foot (B,S,3), x (B,S+1,sdim), status (B,S), iters (B,S), steps_to_goal (B,))."""
+        B, x0, goal, leg, cir, nc, elp, ne = self._inputs(x0, goal, leg, cir, nc, elp, ne)
+        u0 = np.ascontiguousarray(u0, np.float64).reshape(B, self.n)
+        lu = None if last_u is None else np.ascontiguousarray(np.broadcast_to(np.asarray(last_u, np.float64), (B, 2)))
+        S = int(steps)
+        out = dict(foot=np.zeros((B, S, 3)), x=np.zeros((B, S + 1, self.sdim)), status=np.zeros((B, S), np.int32),
+                   iters=np.zeros((B, S), np.int32), steps_to_goal=np.zeros(B, np.int32))
+        rc = self._L.alipmpc_rollout_batch(self._h, B, S, _ptr(x0), _ptr(goal), _ptr(leg), _ptr(cir), _ptr(nc),
+                                           _ptr(elp), _ptr(ne), _ptr(u0), _ptr(lu), _ptr(out["foot"]),
+                                           _ptr(out["x"]), _ptr(out["status"]), _ptr(out["iters"]),
+                                           _ptr(out["steps_to_goal"]), None)
+        self._check(rc, "alipmpc_rollout_batch")
+        return out
+
     # ---------------------------------------------------------------- device (torch) calls
+    def rollout_device(self, inp, out, steps, stream=None):
+        """Asynchronous rollout on device tensors: inp as solve_device, out dict with any of foot (B,S,3),
+        x (B,S+1,sdim), status (B,S), iters (B,S), steps_to_goal (B,)."""
+        import torch
+        st = stream if stream is not None else torch.cuda.current_stream()
+        B = inp["x0"].shape[0]
+        rc = self._L.alipmpc_rollout_batch(
+            self._h, B, int(steps), _ptr(inp["x0"]), _ptr(inp["goal"]), _ptr(inp.get("leg")), _ptr(inp["cir"]),
+            _ptr(inp["nc"]), _ptr(inp.get("elp")), _ptr(inp.get("ne")), _ptr(inp["u0"]), _ptr(inp.get("last_u")),
+            _ptr(out.get("foot")), _ptr(out.get("x")), _ptr(out.get("status")), _ptr(out.get("iters")),
+            _ptr(out.get("steps_to_goal")), _stream_arg(st))
+        self._check(rc, "alipmpc_rollout_batch")
+
     def solve_device(self, inp, out, stream=None):
         """Asynchronous solve on device tensors.  inp/out: dicts of torch CUDA tensors with the shapes of
         solve(); stream: torch.cuda.Stream (defaults to the current stream)."""
@@ -200,7 +242,7 @@ class Solver:
             self._h, B, _ptr(inp["x0"]), _ptr(inp["goal"]), _ptr(inp["leg"]), _ptr(inp["cir"]), _ptr(inp["nc"]),
             _ptr(inp.get("elp")), _ptr(inp.get("ne")), _ptr(inp["u0"]), _ptr(inp.get("last_u")),
             _ptr(out["u"]), _ptr(out.get("foot")), _ptr(out.get("x_pred")), _ptr(out.get("status")),
-            _ptr(out.get("iters")), ctypes.c_void_p(st.cuda_stream))
+            _ptr(out.get("iters")), _stream_arg(st))
         self._check(rc, "alipmpc_solve_batch")
 
     def eval_device(self, inp, out, stream=None):
@@ -212,5 +254,5 @@ class Solver:
             _ptr(inp.get("elp")), _ptr(inp.get("ne")), _ptr(inp["u"]), _ptr(inp.get("last_u")),
             _ptr(out.get("f")), _ptr(out.get("grad")), _ptr(out.get("c")), _ptr(out.get("J")), _ptr(out.get("cl")),
             _ptr(out.get("cu")), _ptr(out.get("goal_eff")), _ptr(out.get("row_active")),
-            ctypes.c_void_p(st.cuda_stream))
+            _stream_arg(st))
         self._check(rc, "alipmpc_eval_batch")

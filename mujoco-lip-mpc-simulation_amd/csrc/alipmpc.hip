@@ -29,7 +29,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/alipmpc.h"
@@ -64,6 +66,7 @@ struct KP {
     const int32_t* ne;
     const double* u0;
     const double* last_u;   // DD: previous control (B x 2)
+    const uint8_t* active;  // nullable: instances with active[b] == 0 are skipped (closed-loop rollouts)
     // solve outputs
     double* u_out;
     double* foot_out;
@@ -997,6 +1000,7 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
     int lane = lane_id();
     const long long b = (long long)blockIdx.x * WAVES_PER_BLOCK + wv;
     if (b >= P.B) return;
+    if (P.active && !P.active[b]) return;   // rollout: instance already at its goal
     // uniform problem sizes in SGPRs (P lives in LDS: a plain read would be a per-lane VGPR value)
     const int mr4 = rfl(P.mr4), mo4 = rfl(P.mo4), m_max = rfl(P.m_max), rps = rfl(P.rps);
     const int nc_max = rfl(P.nc_max), ne_max = rfl(P.ne_max), nobs = nc_max + ne_max;
@@ -2105,6 +2109,7 @@ __global__ __launch_bounds__(256, 4) void dd_solve_kernel(KP Pv)
     int lane = lane_id();
     const long long b = (long long)blockIdx.x * WAVES_PER_BLOCK + wv;
     if (b >= P.B) return;
+    if (P.active && !P.active[b]) return;   // rollout: instance already at its goal
     const int mr4 = rfl(P.mr4), mo4 = rfl(P.mo4), m_max = rfl(P.m_max), rps = rfl(P.rps);
     const int nc_max = rfl(P.nc_max), ne_max = rfl(P.ne_max), nobs = nc_max + ne_max, max_iter = rfl(P.max_iter);
     DDW<N> w = carve_dd<N>(wsb + (size_t)wv * ddw_doubles<N>(nobs, mo4), nobs, mo4);
@@ -2644,6 +2649,106 @@ __global__ __launch_bounds__(256, 4) void dd_eval_kernel(KP Pv)
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// closed-loop rollout ("data_log replay" batch harness): after each solve, every
+// active instance executes its first planned step on an ideal ALIP plant and re-plans from the touchdown
+// state.  One thread per instance (HBM-bound, a few hundred bytes each):
+//   x  <- x_pred[0]                 (= A x + B p_0; the continuous flow get_next_states over a full step,
+//                                     MPC_LIP_modi.py:149-178, evaluated at t_rest = T)
+//   u0 <- warm start from the plan  (modi: the previous x_mpc_tar unshifted, logger_mpc.py:325-331;
+//                                    sig_step: [g2 .. gN, gN], MPC_LIP_sig_step.py:186-189; DD: previous
+//                                    controls, last_u <- first control)
+//   leg <- -leg                     (stance switch, main_sim_mpc.py:111)
+//   close_2_goal: modi |pos_1 - goal| <= 0.15 (MPC_LIP_modi.py:108-115), sig_step any step <= 0.35
+//   (MPC_LIP_sig_step.py:104-111), DD |pos_1 - goal| <= 0.35 (MPC_DD_sig_step.py:92-98); the episode
+//   stops after that step (main_sim_mpc.py:121-131): the instance goes inactive.
+// ------------------------------------------------------------------------------------------------
+struct AdvP {
+    long long B;
+    int t, S, N, sd, n, variant;
+    const double* goal;
+    double* x;        // B x sd     (in/out)
+    double* u0;       // B x n      (in/out)
+    int8_t* leg;      // B          (in/out)
+    double* last_u;   // B x 2      (in/out, DD)
+    const double* u;  // B x n      solve outputs
+    const double* foot;
+    const double* x_pred;
+    const int32_t* status;
+    const int32_t* iters;
+    uint8_t* active;  // B          (in/out)
+    double* foot_traj;     // B x S x 3
+    double* x_traj;        // B x (S+1) x sd
+    int32_t* status_traj;  // B x S
+    int32_t* iters_traj;   // B x S
+    int32_t* steps_to_goal;  // B
+};
+
+__global__ __launch_bounds__(256) void advance_kernel(AdvP A)
+{
+    const long long b = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= A.B) return;
+    const int t = A.t, S = A.S, sd = A.sd, n = A.n, N = A.N;
+    if (!A.active[b]) {
+        if (A.foot_traj)
+            for (int i = 0; i < 3; ++i) A.foot_traj[((size_t)b * S + t) * 3 + i] = NAN;
+        if (A.x_traj)
+            for (int i = 0; i < sd; ++i) A.x_traj[((size_t)b * (S + 1) + t + 1) * sd + i] = A.x[(size_t)b * sd + i];
+        if (A.status_traj) A.status_traj[(size_t)b * S + t] = ALIPMPC_ROLLOUT_DONE;
+        if (A.iters_traj) A.iters_traj[(size_t)b * S + t] = 0;
+        return;
+    }
+    const double* xp = A.x_pred + (size_t)b * N * sd;
+    if (A.foot_traj)
+        for (int i = 0; i < 3; ++i) A.foot_traj[((size_t)b * S + t) * 3 + i] = A.foot[3 * b + i];
+    if (A.status_traj) A.status_traj[(size_t)b * S + t] = A.status[b];
+    if (A.iters_traj) A.iters_traj[(size_t)b * S + t] = A.iters[b];
+    for (int i = 0; i < sd; ++i) {
+        A.x[(size_t)b * sd + i] = xp[i];
+        if (A.x_traj) A.x_traj[((size_t)b * (S + 1) + t + 1) * sd + i] = xp[i];
+    }
+    const double* ub = A.u + (size_t)b * n;
+    double* u0 = A.u0 + (size_t)b * n;
+    if (A.variant == ALIPMPC_VARIANT_SIG_STEP) {
+        const int blk = n / N;
+        for (int k = 0; k < N; ++k) {
+            const int src = k + 1 < N ? k + 1 : N - 1;
+            for (int i = 0; i < blk; ++i) u0[k * blk + i] = ub[src * blk + i];
+        }
+    } else {
+        for (int i = 0; i < n; ++i) u0[i] = ub[i];
+    }
+    if (A.variant == ALIPMPC_VARIANT_DD) {
+        A.last_u[2 * b] = ub[0];
+        A.last_u[2 * b + 1] = ub[1];
+    } else {
+        A.leg[b] = (int8_t)(-A.leg[b]);
+    }
+    const double gx_ = A.goal[2 * b], gy_ = A.goal[2 * b + 1];
+    bool close = false;
+    const int kmax = A.variant == ALIPMPC_VARIANT_SIG_STEP ? N : 1;
+    const double rad = A.variant == ALIPMPC_VARIANT_MODI ? 0.15 : 0.35;
+    for (int k = 0; k < kmax; ++k) {
+        const double dx = xp[k * sd] - gx_, dy = xp[k * sd + 1] - gy_;
+        close = close || sqrt(dx * dx + dy * dy) <= rad;
+    }
+    if (close) {
+        A.active[b] = 0;
+        if (A.steps_to_goal) A.steps_to_goal[b] = t + 1;
+    }
+}
+
+__global__ __launch_bounds__(256) void rollout_init_kernel(long long B, int S, int sd, const double* x0, double* xtraj,
+                                                           uint8_t* active, int32_t* steps_to_goal)
+{
+    const long long b = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    active[b] = 1;
+    if (steps_to_goal) steps_to_goal[b] = -1;
+    if (xtraj)
+        for (int i = 0; i < sd; ++i) xtraj[(size_t)b * (S + 1) * sd + i] = x0[(size_t)b * sd + i];
+}
+
 }  // namespace alip
 
 // ================================================================================================
@@ -2665,8 +2770,15 @@ struct Handle {
     // staging for host-pointer calls
     void* stage = nullptr;
     size_t stage_bytes = 0;
+    // rollout working set (evolving state, warm starts, per-step solve outputs)
+    void* rstage = nullptr;
+    size_t rstage_bytes = 0;
     hipStream_t own = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // launch timing: a ring of event pairs, so a re-record never targets an event still pending on the
+    // stream (that serialises the host with the previous launch)
+    static constexpr int NEV = 16;
+    hipEvent_t ev[NEV][2] = {};
+    int evi = 0, evlast = -1;
     bool timed = false;
     std::string err;
 };
@@ -2831,6 +2943,22 @@ KP make_kp(const Handle* h, long long B, bool solve)
     return P;
 }
 
+// dynamic-LDS opt-in, once per kernel and size (hipFuncSetAttribute is a host round trip: keep it out of the
+// steady-state launch path)
+void set_smem(const void* f, size_t smem)
+{
+    static std::mutex mtx;
+    static std::unordered_map<const void*, size_t> done[64];   // per device ordinal
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(mtx);
+    auto& d = done[dev & 63];
+    auto it = d.find(f);
+    if (it != d.end() && it->second >= smem) return;
+    (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    d[f] = smem;
+}
+
 // J-layout steps (4 rows each) of the compiled solve kernels; mo4 is rounded up to 4 * ksm_of(rows)
 int ksm_of(int rows)
 {
@@ -2847,7 +2975,7 @@ hipError_t launch_t(bool solve, const KP& P, size_t smem, hipStream_t st)
     if (solve) {
         // KSM = 4-row steps of the J layout, the smallest compiled size covering mo4 rows
         auto go = [&](auto kern) {
-            (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+            set_smem((const void*)kern, smem);
             hipLaunchKernelGGL(kern, dim3(grid), dim3(WAVE * WAVES_PER_BLOCK), smem, st, P);
         };
         if (P.mo4 <= 32)
@@ -2865,7 +2993,7 @@ hipError_t launch_t(bool solve, const KP& P, size_t smem, hipStream_t st)
         else
             go(solve_kernel<N, 48>);
     } else {
-        (void)hipFuncSetAttribute((const void*)eval_kernel<N>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        set_smem((const void*)eval_kernel<N>, smem);
         hipLaunchKernelGGL(eval_kernel<N>, dim3(grid), dim3(WAVE * WAVES_PER_BLOCK), smem, st, P);
     }
     return hipGetLastError();
@@ -2876,7 +3004,7 @@ hipError_t launch_dd(bool solve, const KP& P, size_t smem, hipStream_t st)
 {
     const unsigned grid = (unsigned)((P.B + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
     auto go = [&](auto kern) {
-        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        set_smem((const void*)kern, smem);
         hipLaunchKernelGGL(kern, dim3(grid), dim3(WAVE * WAVES_PER_BLOCK), smem, st, P);
     };
     if (!solve)
@@ -2913,6 +3041,23 @@ hipError_t launch(const Handle* h, bool solve, const KP& P, hipStream_t st)
     case 6: return launch_t<6>(solve, P, smem, st);
     }
     return hipErrorInvalidValue;
+}
+
+// hip_stream argument -> the stream to launch on (NULL = host-pointer mode on the handle's own stream,
+// ALIPMPC_STREAM_NULL = device pointers on the null stream)
+hipStream_t stream_of(const Handle* h, void* hip_stream)
+{
+    if (!hip_stream) return h->own;
+    if (hip_stream == ALIPMPC_STREAM_NULL) return nullptr;
+    return (hipStream_t)hip_stream;
+}
+
+bool create_events(Handle* h)
+{
+    for (auto& pr : h->ev)
+        for (hipEvent_t& e : pr)
+            if (hipEventCreate(&e) != hipSuccess) return false;
+    return true;
 }
 
 int ensure_stage(Handle* h, size_t bytes)
@@ -3062,7 +3207,7 @@ int alipmpc_create(const alipmpc_cfg* cfg, int device, void** handle)
     };
     if (!up(&h->dGp, Gp) || !up(&h->dEp, Ep) || !up(&h->dGu, Gu) || !up(&h->dEu, Eu) ||
         hipStreamCreateWithFlags(&h->own, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess) {
+        !create_events(h)) {
         alipmpc_destroy(h);
         return ALIPMPC_EHIP;
     }
@@ -3093,16 +3238,19 @@ static int run_batch(Handle* h, bool solve, int64_t B, const double* x0, const d
     const int N = h->N, n = dd ? 2 * N : 5 * N, sd = dd ? 3 : 5;
     const size_t mm_ = (size_t)h->m_max;
     KP P = make_kp(h, B, solve);
-    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : h->own;
+    hipStream_t st = stream_of(h, hip_stream);
     if (hip_stream) {
         P.x0 = x0; P.goal = goal; P.leg = leg; P.cir = cir; P.nc = nc; P.elp = elp; P.ne = ne; P.u0 = u0;
         P.last_u = last_u;
         P.u_out = u_out; P.foot_out = foot_out; P.x_pred = x_pred; P.status = status; P.iters = iters;
         P.f_out = f; P.grad_out = grad; P.c_out = c; P.J_out = J; P.cl_out = cl; P.cu_out = cu;
         P.goal_eff_out = goal_eff; P.active_out = row_active;
-        HIPCHK(h, hipEventRecord(h->ev0, st));
+        const int ei = h->evi;
+        h->evi = (ei + 1) % Handle::NEV;
+        HIPCHK(h, hipEventRecord(h->ev[ei][0], st));
         HIPCHK(h, launch(h, solve, P, st));
-        HIPCHK(h, hipEventRecord(h->ev1, st));
+        HIPCHK(h, hipEventRecord(h->ev[ei][1], st));
+        h->evlast = ei;
         h->timed = true;
         return ALIPMPC_OK;
     }
@@ -3166,9 +3314,12 @@ static int run_batch(Handle* h, bool solve, int64_t B, const double* x0, const d
         P.f_out = d_f; P.grad_out = d_g; P.c_out = d_c; P.J_out = J ? d_J : nullptr; P.cl_out = d_cl; P.cu_out = d_cu;
         P.goal_eff_out = d_ge; P.active_out = d_ra;
     }
-    HIPCHK(h, hipEventRecord(h->ev0, st));
+    const int ei = h->evi;
+    h->evi = (ei + 1) % Handle::NEV;
+    HIPCHK(h, hipEventRecord(h->ev[ei][0], st));
     HIPCHK(h, launch(h, solve, P, st));
-    HIPCHK(h, hipEventRecord(h->ev1, st));
+    HIPCHK(h, hipEventRecord(h->ev[ei][1], st));
+    h->evlast = ei;
     h->timed = true;
     if (solve) {
         HIPCHK(h, d2h(u_out, d_u, Bz * n * 8));
@@ -3208,6 +3359,125 @@ int alipmpc_eval_batch(void* handle, int64_t B, const double* x0, const double* 
                      nullptr, nullptr, f, grad, c, J, cl, cu, goal_eff, row_active, hip_stream);
 }
 
+int alipmpc_rollout_batch(void* handle, int64_t B, int32_t S, const double* x0, const double* goal, const int8_t* leg,
+                          const double* cir, const int32_t* nc, const double* elp, const int32_t* ne, const double* u0,
+                          const double* last_u, double* foot_traj, double* x_traj, int32_t* status_traj,
+                          int32_t* iters_traj, int32_t* steps_to_goal, void* hip_stream)
+{
+    Handle* h = (Handle*)handle;
+    if (!h) return ALIPMPC_EINVAL;
+    if (B < 0 || S < 0) return fail(h, ALIPMPC_EINVAL, "B < 0 or S < 0");
+    if (B == 0 || S == 0) return ALIPMPC_OK;
+    const alipmpc_cfg& cf = h->cfg;
+    const bool dd = cf.variant == ALIPMPC_VARIANT_DD;
+    if (!x0 || !goal || (!leg && !dd) || !nc || !u0 || (cf.nc_max > 0 && !cir) || (cf.ne_max > 0 && (!elp || !ne)))
+        return fail(h, ALIPMPC_EINVAL, "missing input pointer");
+    HIPCHK(h, hipSetDevice(h->device));
+    const int N = h->N, n = dd ? 2 * N : 5 * N, sd = dd ? 3 : 5;
+    const size_t Bz = (size_t)B, Sz = (size_t)S;
+    hipStream_t st = stream_of(h, hip_stream);
+    const bool host = hip_stream == nullptr;   // ALIPMPC_STREAM_NULL: device pointers, null stream
+    // working set (+ staged inputs / outputs for host-pointer calls)
+    auto layout = [&](Carver& cv, bool take_io) {
+        struct L {
+            double *x, *u0, *lu, *u, *foot, *xp;
+            int8_t* leg;
+            int32_t *st, *it;
+            uint8_t* act;
+            double *goal, *cir, *elp, *ft, *xt;
+            int32_t *nc, *ne, *stt, *itt, *sg;
+        } l{};
+        l.x = cv.take<double>(Bz * sd); l.u0 = cv.take<double>(Bz * n); l.lu = cv.take<double>(Bz * 2);
+        l.u = cv.take<double>(Bz * n); l.foot = cv.take<double>(Bz * 3); l.xp = cv.take<double>(Bz * N * sd);
+        l.leg = cv.take<int8_t>(Bz); l.st = cv.take<int32_t>(Bz); l.it = cv.take<int32_t>(Bz);
+        l.act = cv.take<uint8_t>(Bz);
+        if (take_io) {
+            l.goal = cv.take<double>(Bz * 2); l.cir = cv.take<double>(Bz * 3 * cf.nc_max);
+            l.elp = cv.take<double>(Bz * 5 * cf.ne_max); l.nc = cv.take<int32_t>(Bz); l.ne = cv.take<int32_t>(Bz);
+            l.ft = cv.take<double>(Bz * Sz * 3); l.xt = cv.take<double>(Bz * (Sz + 1) * sd);
+            l.stt = cv.take<int32_t>(Bz * Sz); l.itt = cv.take<int32_t>(Bz * Sz); l.sg = cv.take<int32_t>(Bz);
+        }
+        return l;
+    };
+    size_t need;
+    {
+        Carver cv{nullptr};
+        layout(cv, host);
+        need = cv.off + 256;
+    }
+    if (h->rstage_bytes < need) {
+        if (h->rstage) hipFree(h->rstage);
+        h->rstage = nullptr;
+        h->rstage_bytes = 0;
+        HIPCHK(h, hipMalloc(&h->rstage, need));
+        h->rstage_bytes = need;
+    }
+    Carver cv{(char*)h->rstage};
+    auto l = layout(cv, host);
+    const hipMemcpyKind in_kind = host ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
+    HIPCHK(h, hipMemcpyAsync(l.x, x0, Bz * sd * 8, in_kind, st));
+    HIPCHK(h, hipMemcpyAsync(l.u0, u0, Bz * n * 8, in_kind, st));
+    if (leg) HIPCHK(h, hipMemcpyAsync(l.leg, leg, Bz, in_kind, st));
+    if (last_u)
+        HIPCHK(h, hipMemcpyAsync(l.lu, last_u, Bz * 2 * 8, in_kind, st));
+    else
+        HIPCHK(h, hipMemsetAsync(l.lu, 0, Bz * 2 * 8, st));
+    const double *d_goal = goal, *d_cir = cir, *d_elp = elp;
+    const int32_t *d_nc = nc, *d_ne = ne;
+    double *d_ft = foot_traj, *d_xt = x_traj;
+    int32_t *d_stt = status_traj, *d_itt = iters_traj, *d_sg = steps_to_goal;
+    if (host) {
+        HIPCHK(h, hipMemcpyAsync(l.goal, goal, Bz * 2 * 8, hipMemcpyHostToDevice, st));
+        if (cf.nc_max) HIPCHK(h, hipMemcpyAsync(l.cir, cir, Bz * 3 * cf.nc_max * 8, hipMemcpyHostToDevice, st));
+        HIPCHK(h, hipMemcpyAsync(l.nc, nc, Bz * 4, hipMemcpyHostToDevice, st));
+        if (cf.ne_max) {
+            HIPCHK(h, hipMemcpyAsync(l.elp, elp, Bz * 5 * cf.ne_max * 8, hipMemcpyHostToDevice, st));
+            HIPCHK(h, hipMemcpyAsync(l.ne, ne, Bz * 4, hipMemcpyHostToDevice, st));
+        }
+        d_goal = l.goal; d_cir = l.cir; d_nc = l.nc;
+        d_elp = cf.ne_max ? l.elp : nullptr;
+        d_ne = cf.ne_max ? l.ne : nullptr;
+        d_ft = foot_traj ? l.ft : nullptr; d_xt = x_traj ? l.xt : nullptr;
+        d_stt = status_traj ? l.stt : nullptr; d_itt = iters_traj ? l.itt : nullptr;
+        d_sg = steps_to_goal ? l.sg : nullptr;
+    }
+    const unsigned g1 = (unsigned)((B + 255) / 256);
+    hipLaunchKernelGGL(rollout_init_kernel, dim3(g1), dim3(256), 0, st, (long long)B, (int)S, sd, (const double*)l.x,
+                       d_xt, l.act, d_sg);
+    HIPCHK(h, hipGetLastError());
+    KP P = make_kp(h, B, true);
+    P.goal = d_goal; P.cir = d_cir; P.nc = d_nc; P.elp = d_elp; P.ne = d_ne;
+    P.x0 = l.x; P.leg = dd ? nullptr : l.leg; P.u0 = l.u0; P.last_u = dd ? l.lu : nullptr; P.active = l.act;
+    P.u_out = l.u; P.foot_out = l.foot; P.x_pred = l.xp; P.status = l.st; P.iters = l.it;
+    AdvP A;
+    std::memset(&A, 0, sizeof(A));
+    A.B = B; A.S = S; A.N = N; A.sd = sd; A.n = n; A.variant = cf.variant; A.goal = d_goal;
+    A.x = l.x; A.u0 = l.u0; A.leg = l.leg; A.last_u = l.lu; A.u = l.u; A.foot = l.foot; A.x_pred = l.xp;
+    A.status = l.st; A.iters = l.it; A.active = l.act;
+    A.foot_traj = d_ft; A.x_traj = d_xt; A.status_traj = d_stt; A.iters_traj = d_itt; A.steps_to_goal = d_sg;
+    const int ei = h->evi;
+    h->evi = (ei + 1) % Handle::NEV;
+    HIPCHK(h, hipEventRecord(h->ev[ei][0], st));
+    for (int t = 0; t < S; ++t) {
+        HIPCHK(h, launch(h, true, P, st));
+        A.t = t;
+        hipLaunchKernelGGL(advance_kernel, dim3(g1), dim3(256), 0, st, A);
+        HIPCHK(h, hipGetLastError());
+    }
+    HIPCHK(h, hipEventRecord(h->ev[ei][1], st));
+    h->evlast = ei;
+    h->timed = true;
+    if (host) {
+        if (foot_traj) HIPCHK(h, hipMemcpyAsync(foot_traj, l.ft, Bz * Sz * 3 * 8, hipMemcpyDeviceToHost, st));
+        if (x_traj) HIPCHK(h, hipMemcpyAsync(x_traj, l.xt, Bz * (Sz + 1) * sd * 8, hipMemcpyDeviceToHost, st));
+        if (status_traj) HIPCHK(h, hipMemcpyAsync(status_traj, l.stt, Bz * Sz * 4, hipMemcpyDeviceToHost, st));
+        if (iters_traj) HIPCHK(h, hipMemcpyAsync(iters_traj, l.itt, Bz * Sz * 4, hipMemcpyDeviceToHost, st));
+        if (steps_to_goal) HIPCHK(h, hipMemcpyAsync(steps_to_goal, l.sg, Bz * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(h, hipStreamSynchronize(st));
+    }
+    return ALIPMPC_OK;
+}
+
 #ifdef ALIP_STAMPS
 int alipmpc_dbg_stamps(unsigned long long* out, int reset)
 {
@@ -3225,9 +3495,11 @@ double alipmpc_last_kernel_ms(void* handle)
 {
     Handle* h = (Handle*)handle;
     if (!h || !h->timed) return 0.0;
-    if (hipEventSynchronize(h->ev1) != hipSuccess) return 0.0;
+    if (h->evlast < 0) return 0.0;
+    hipEvent_t e0 = h->ev[h->evlast][0], e1 = h->ev[h->evlast][1];
+    if (hipEventSynchronize(e1) != hipSuccess) return 0.0;
     float ms = 0.f;
-    if (hipEventElapsedTime(&ms, h->ev0, h->ev1) != hipSuccess) return 0.0;
+    if (hipEventElapsedTime(&ms, e0, e1) != hipSuccess) return 0.0;
     return (double)ms;
 }
 
@@ -3246,8 +3518,10 @@ void alipmpc_destroy(void* handle)
     for (double* d : {h->dGp, h->dEp, h->dGu, h->dEu})
         if (d) (void)hipFree(d);
     if (h->stage) hipFree(h->stage);
-    if (h->ev0) hipEventDestroy(h->ev0);
-    if (h->ev1) hipEventDestroy(h->ev1);
+    if (h->rstage) hipFree(h->rstage);
+    for (auto& pr : h->ev)
+        for (hipEvent_t e : pr)
+            if (e) hipEventDestroy(e);
     if (h->own) hipStreamDestroy(h->own);
     delete h;
 }

@@ -165,3 +165,69 @@ def eval_batch_dd(cfg, x0, goal, cir, nc, elp, ne, u, last_u):
     if rc != 0:
         raise RuntimeError(f"oracle_eval_batch_dd failed: {rc}")
     return out
+
+
+def rollout_batch(cfg, x0, goal, leg, cir, nc, elp, ne, u0, last_u=None, steps=8, nthreads=1):
+    """Closed-loop receding-horizon rollout on an ideal ALIP plant (oracle of alipmpc_rollout_batch).
+    Per step: solve the active instances (C oracle); x <- x_pred[0] (the touchdown state = get_next_states
+    over a full step, MPC_LIP_modi.py:149-178); stance switch leg <- -leg (main_sim_mpc.py:111); warm start
+    modi: previous x_mpc_tar unshifted (logger_mpc.py:325-331), sig_step: [g2..gN, gN]
+    (MPC_LIP_sig_step.py:186-189), DD: previous controls + last_u <- first control; retire after
+    close_2_goal (modi |pos_1-goal| <= 0.15, MPC_LIP_modi.py:108-115; sig_step any step <= 0.35,
+    MPC_LIP_sig_step.py:104-111; DD |pos_1-goal| <= 0.35, MPC_DD_sig_step.py:92-98; the episode stops after
+    that step, main_sim_mpc.py:121-131)."""
+    dd = cfg.variant == VARIANT_DD
+    sd = 3 if dd else 5
+    N, n = cfg.N, n_vars(cfg)
+    x = np.array(x0, np.float64).reshape(-1, sd).copy()
+    B = len(x)
+    goal = np.ascontiguousarray(np.broadcast_to(np.asarray(goal, np.float64), (B, 2)))
+    u0 = np.array(u0, np.float64).reshape(B, n).copy()
+    legv = None if dd else np.array(leg, np.int8).reshape(B).copy()
+    lu = np.zeros((B, 2)) if last_u is None else np.array(np.broadcast_to(np.asarray(last_u, np.float64), (B, 2)))
+    S = int(steps)
+    foot = np.full((B, S, 3), np.nan)
+    xs = np.zeros((B, S + 1, sd))
+    xs[:, 0] = x
+    status = np.full((B, S), -10, np.int32)
+    iters = np.zeros((B, S), np.int32)
+    stg = np.full(B, -1, np.int32)
+    active = np.ones(B, bool)
+    elp_a = None if elp is None else np.asarray(elp)
+    ne_a = None if ne is None else np.asarray(ne)
+    for t in range(S):
+        idx = np.nonzero(active)[0]
+        if len(idx):
+            sub = lambda a: None if a is None else np.asarray(a)[idx]
+            if dd:
+                o = solve_batch_dd(cfg, x[idx], goal[idx], sub(cir), sub(nc), sub(elp_a), sub(ne_a), u0[idx], lu[idx],
+                                   nthreads=nthreads)
+            else:
+                o = solve_batch(cfg, x[idx], goal[idx], legv[idx], sub(cir), sub(nc), sub(elp_a), sub(ne_a), u0[idx],
+                                nthreads=nthreads)
+            foot[idx, t] = o["foot"]
+            status[idx, t] = o["status"]
+            iters[idx, t] = o["iters"]
+            xp = o["x_pred"]
+            x[idx] = xp[:, 0]
+            u = o["u"]
+            if cfg.variant == VARIANT_SIG_STEP:
+                blk = n // N
+                ub = u.reshape(len(idx), N, blk)
+                u0[idx] = np.concatenate([ub[:, 1:], ub[:, -1:]], axis=1).reshape(len(idx), n)
+            else:
+                u0[idx] = u
+            if dd:
+                lu[idx] = u[:, 0:2]
+            else:
+                legv[idx] = -legv[idx]
+            d = np.sqrt(((xp[:, :, 0:2] - goal[idx, None, :]) ** 2).sum(-1))
+            if cfg.variant == VARIANT_SIG_STEP:
+                close = (d <= 0.35).any(1)
+            else:
+                close = d[:, 0] <= (0.15 if cfg.variant == VARIANT_MODI else 0.35)
+            done = idx[close]
+            active[done] = False
+            stg[done] = t + 1
+        xs[:, t + 1] = x
+    return dict(foot=foot, x=xs, status=status, iters=iters, steps_to_goal=stg)

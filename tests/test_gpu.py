@@ -311,3 +311,60 @@ def test_planner_dropins_match_batched_solver(gpu_lib, golden):
     assert fesi == db["status"][0] and len(states) == 4 and len(control) == 3
     assert np.max(np.abs(np.array(states[1:]) - db["x_pred"][0])) < 1e-12
     assert np.max(np.abs(np.ravel(control) - db["u"][0])) < 1e-15
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2])
+def test_rollout_matches_oracle(gpu_lib, coracle, variant):
+    """alipmpc_rollout_batch (S solve launches + plant-update kernels on one stream) against the oracle's
+    closed loop on the same seeded episodes: whole trajectories (footholds, touchdown states, statuses,
+    steps to goal) agree on the large majority of episodes (a rounding-level difference can switch a
+    nonconvex solve into another basin and the episode then diverges)."""
+    from alipmpc import scenes
+    dd = variant == 2
+    N, B, S = 3, 128, 6
+    bt = scenes.make_batch(B, seed=91 + variant, n_cir=5, N=N)
+    if dd:
+        x0 = bt["x0"][:, [0, 1, 4]].copy()
+        u0 = np.tile([0.6, 0.0], (B, N))
+        lu = np.tile([0.6, 0.0], (B, 1))
+    else:
+        x0, lu = bt["x0"].copy(), None
+    x0[:16, 0:2] = bt["goal"][:16] - np.array([0.3, 0.2])
+    if not dd:
+        u0 = np.tile(x0, (1, N))
+    cfg = gpu_lib.default_cfg(variant, N, nc_max=5, ne_max=0)
+    s = gpu_lib.Solver(cfg)
+    o = s.rollout(x0, bt["goal"], None if dd else bt["leg"], bt["cir"], bt["nc"], u0=u0, last_u=lu, steps=S)
+    ref = coracle.rollout_batch(coracle.default_cfg(variant, N, nc_max=5, ne_max=0), x0, bt["goal"], bt["leg"],
+                                bt["cir"], bt["nc"], None, None, u0, lu, steps=S, nthreads=8)
+    same_status = (o["status"] == ref["status"]).all(1)
+    fo = np.nan_to_num(o["foot"], nan=1e9)
+    fr = np.nan_to_num(ref["foot"], nan=1e9)
+    same_path = (np.abs(fo - fr) <= 1e-4 * np.maximum(1.0, np.abs(fr))).all((1, 2)) & \
+        (np.abs(o["x"] - ref["x"]) <= 1e-4 * np.maximum(1.0, np.abs(ref["x"]))).all((1, 2))
+    agree = (same_status & same_path).mean()
+    assert agree >= 0.85, agree
+    assert (o["steps_to_goal"] == ref["steps_to_goal"]).mean() >= 0.9
+    assert (o["steps_to_goal"][:16] > 0).sum() >= 8
+    # retired instances are not solved again
+    for b in np.nonzero(o["steps_to_goal"] > 0)[0]:
+        assert (o["status"][b, o["steps_to_goal"][b]:] == gpu_lib.ROLLOUT_DONE).all()
+    # device-pointer path gives the same trajectories
+    import torch
+    dev = torch.device("cuda", 0)
+    inp = {"x0": torch.from_numpy(x0).to(dev), "goal": torch.from_numpy(bt["goal"]).to(dev),
+           "cir": torch.from_numpy(bt["cir"]).to(dev), "nc": torch.from_numpy(bt["nc"].astype(np.int32)).to(dev),
+           "u0": torch.from_numpy(u0).to(dev)}
+    if dd:
+        inp["last_u"] = torch.from_numpy(lu).to(dev)
+    else:
+        inp["leg"] = torch.from_numpy(bt["leg"].astype(np.int8)).to(dev)
+    out = {"foot": torch.empty((B, S, 3), dtype=torch.float64, device=dev),
+           "x": torch.empty((B, S + 1, x0.shape[1]), dtype=torch.float64, device=dev),
+           "status": torch.empty((B, S), dtype=torch.int32, device=dev),
+           "steps_to_goal": torch.empty((B,), dtype=torch.int32, device=dev)}
+    s.rollout_device(inp, out, S)
+    torch.cuda.synchronize()
+    assert np.array_equal(out["status"].cpu().numpy(), o["status"])
+    assert np.array_equal(np.nan_to_num(out["foot"].cpu().numpy(), nan=7.0), np.nan_to_num(o["foot"], nan=7.0))
+    assert np.array_equal(out["steps_to_goal"].cpu().numpy(), o["steps_to_goal"])

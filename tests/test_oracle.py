@@ -224,3 +224,54 @@ def test_dd_solutions_match_scipy_goldens(golden, coracle):
         assert st == r["status"][t]
         if st == 0:
             assert np.max(np.abs(u - r["u"][t])) < 1e-6
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2])
+def test_rollout_oracle_semantics(coracle, variant):
+    """Closed-loop rollout: step 0 is the plain solve, the plant executes the first planned
+    step (x <- x_pred[0] = A x + B p_0, i.e. get_next_states over a full step), stance and warm start follow
+    the reference drivers, and a goal-reached instance is retired."""
+    import sys
+    import math
+    from alipmpc import scenes
+    from alipmpc.planner import next_state
+    dd = variant == 2
+    N = 3
+    bt = scenes.make_batch(24, seed=31 + variant, n_cir=3, N=N)
+    cfg = coracle.default_cfg(variant, N, nc_max=3, ne_max=0)
+    if dd:
+        x0 = bt["x0"][:, [0, 1, 4]]
+        u0 = np.tile([0.6, 0.0], (24, N))
+        lu = np.tile([0.6, 0.0], (24, 1))
+    else:
+        x0, u0, lu = bt["x0"], bt["u0"], None
+    # put a few instances right next to the goal so that they retire inside the horizon
+    x0 = x0.copy()
+    x0[:4, 0:2] = bt["goal"][:4] - np.array([0.25, 0.25])
+    if not dd:
+        u0 = np.tile(x0, (1, N))
+    ro = coracle.rollout_batch(cfg, x0, bt["goal"], bt["leg"], bt["cir"], bt["nc"], None, None, u0, lu, steps=4,
+                               nthreads=4)
+    if dd:
+        first = coracle.solve_batch_dd(cfg, x0, bt["goal"], bt["cir"], bt["nc"], None, None, u0, lu)
+    else:
+        first = coracle.solve_batch(cfg, x0, bt["goal"], bt["leg"], bt["cir"], bt["nc"], None, None, u0)
+    assert np.array_equal(ro["foot"][:, 0], first["foot"])
+    assert np.array_equal(ro["status"][:, 0], first["status"])
+    assert np.array_equal(ro["x"][:, 1], first["x_pred"][:, 0])
+    beta = math.sqrt(9.81)
+    for b in range(24):
+        for t in range(4):
+            if ro["status"][b, t] == -10:
+                assert np.isnan(ro["foot"][b, t]).all()
+                assert np.array_equal(ro["x"][b, t + 1], ro["x"][b, t])
+                continue
+            if not dd:   # ideal ALIP plant == the reference's continuous flow over a full step
+                xs = ro["x"][b, t]
+                xn, _ = next_state(beta, 0.4, xs[0:2], xs[2:4], xs[4], ro["foot"][b, t], 0.4)
+                assert np.allclose(xn, ro["x"][b, t + 1], rtol=0, atol=1e-12)
+    reached = ro["steps_to_goal"] > 0
+    assert reached[:4].any()
+    for b in np.nonzero(reached)[0]:
+        k = ro["steps_to_goal"][b]
+        assert (ro["status"][b, k:] == -10).all() and (ro["status"][b, :k] != -10).all()
