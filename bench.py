@@ -1,14 +1,20 @@
 #!/usr/bin/env python3
 """Benchmark: batched ALIP-MPC-CBF solves/sec on MI355X (BASELINE.json metric).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--variant modi] [--horizon 3]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4|cfg5] [--batch B] ...
 
 One "step" = one fused interior-point solve of a batch of B independent NLP instances whose inputs are
 already resident in HBM (one launch of solve_kernel through the C ABI on the current HIP stream).
 Default workload = BASELINE configs[1] ("cfg2"): B = 4096 random ALIP initial states per GPU, N = 3,
 5 circular obstacles, fp64.  For N > 1 GPUs (torchrun, one process per GPU, RCCL) every rank solves its
-own 4096-instance shard (weak scaling; scenes are generated from (seed, rank)) and each step ends with
-one RCCL gather of the per-instance outputs to rank 0 — the path has no other exchange.
+own shard (scenes are generated from (seed, rank)) and each step ends with one RCCL gather of the
+per-instance outputs to rank 0 — the path has no other exchange.
+The other BASELINE configs are presets (not the driver's default line):
+  cfg3  B = 65,536 per GPU, N = 5, 5 circles + 5 ellipses, fp64 (weak scaling)
+  cfg4  262,144 instances in total sharded over the GPUs, N = 3, 5 circles, fp64 (strong scaling)
+  cfg5  1,048,576 randomized scenes in total (one obstacle field each), N = 3, fp32 solve kernels;
+        also reports the feasible fraction (solutions re-evaluated by the fp64 reference callbacks, no
+        active row violated by more than 1e-4; counts all-reduced over ranks)
 
 Prints ONE JSON line on rank 0 (see DESIGN.md §Measurement for the roofline / cpu_baseline fields).
 """
@@ -26,6 +32,15 @@ sys.path.insert(0, os.path.join(ROOT, "mujoco-lip-mpc-simulation_amd"))
 # per-IP-iteration algorithmic work of one instance: KKT GEMM J^T Sigma J (2 m n^2) +
 # Cholesky and two triangular solves (n^3/3 + 2 n^2) + NLP evaluation (rollout, f, grad, c, J)
 FP64_PEAK_TFLOPS = 78.6      # MI355X FP64 matrix / vector peak (AMD spec; MI355X_MICROARCH.md lists no FP64 row)
+FP32_PEAK_TFLOPS = 157.3     # MI355X FP32 matrix = vector peak (MI355X_MICROARCH.md)
+
+# BASELINE.json configs: (instances, per_gpu?, horizon, circles, ellipses, precision, distinct fields)
+CONFIGS = {
+    "cfg2": dict(batch=4096, per_gpu=True, horizon=3, circles=5, ellipses=0, fp32=False),
+    "cfg3": dict(batch=65536, per_gpu=True, horizon=5, circles=5, ellipses=5, fp32=False),
+    "cfg4": dict(batch=262144, per_gpu=False, horizon=3, circles=5, ellipses=0, fp32=False),
+    "cfg5": dict(batch=1048576, per_gpu=False, horizon=3, circles=5, ellipses=0, fp32=True),
+}
 HBM_PEAK_GBS = 8000.0
 
 
@@ -36,13 +51,13 @@ def flops_per_iter(n, m, N, nobs):
     return kkt + chol + nlp
 
 
-def solve_kernel_name(N, rps, modi):
+def solve_kernel_name(N, rps, modi, fp32=False):
     """The solve_kernel<N, KSM> instance the library dispatches (csrc/alipmpc.hip: ksm_of): constraint rows
     in the solve layout (f_en split into two rows for modi) + N objective rows, in 4-row J-layout steps."""
     m = N * (rps + (1 if modi else 0))
     rows = ((m + 3) // 4) * 4 + 4 * ((N + 3) // 4)
     ksm = next(k for k in (8, 10, 12, 16, 24, 32, 48) if rows <= 4 * k)
-    return f"solve_kernel<{N},{ksm}>", m
+    return f"solve_kernel<{N},{ksm},{'float' if fp32 else 'double'}>", m
 
 
 def parse():
@@ -50,10 +65,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=4096, help="instances per GPU")
+    ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
+    ap.add_argument("--batch", type=int, default=None, help="instances per GPU (default: the config's)")
     ap.add_argument("--variant", default="modi", choices=["modi", "sig_step"])
-    ap.add_argument("--horizon", type=int, default=3)
-    ap.add_argument("--obstacles", type=int, default=5)
+    ap.add_argument("--horizon", type=int, default=None)
+    ap.add_argument("--obstacles", type=int, default=None, help="circles per instance")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -81,11 +97,26 @@ def main():
         raise SystemExit("bench.py needs a visible MI355X (torch.cuda.is_available() is False)")
 
     variant = {"modi": alipmpc.VARIANT_MODI, "sig_step": alipmpc.VARIANT_SIG_STEP}[args.variant]
-    N = args.horizon
-    cfg = alipmpc.default_cfg(variant, N, nc_max=args.obstacles, ne_max=0)
+    preset = CONFIGS[args.config]
+    N = args.horizon or preset["horizon"]
+    n_cir = preset["circles"] if args.obstacles is None else args.obstacles
+    n_elp = preset["ellipses"]
+    fp32 = preset["fp32"]
+    if args.batch is not None:
+        B = args.batch
+    elif preset["per_gpu"]:
+        B = preset["batch"]
+    else:   # a fixed total sharded over the ranks (contiguous shards; the last rank takes the remainder)
+        B = preset["batch"] // world + (preset["batch"] % world if rank == world - 1 else 0)
+    prec = {"precision": alipmpc.PREC_FP32} if fp32 else {}
+    cfg = alipmpc.default_cfg(variant, N, nc_max=n_cir, ne_max=n_elp, **prec)
     solver = alipmpc.Solver(cfg, device=dev.index)
-    B = args.batch
-    batch = scenes.make_batch(B, seed=args.seed * 1000 + rank, n_cir=args.obstacles, N=N)
+    seed = args.seed * 1000 + rank
+    if args.config == "cfg2":
+        batch = scenes.make_batch(B, seed=seed, n_cir=n_cir, N=N)
+    else:   # vectorised generator: one obstacle field per instance (cfg3: 4096 shared fields)
+        batch = scenes.make_batch_vec(B, seed=seed, n_cir=n_cir, n_elp=n_elp, N=N,
+                                      fields=4096 if args.config == "cfg3" else None)
     n = solver.n
     inp = {
         "x0": torch.from_numpy(batch["x0"]).to(dev),
@@ -95,6 +126,9 @@ def main():
         "nc": torch.from_numpy(batch["nc"].astype(np.int32)).to(dev),
         "u0": torch.from_numpy(batch["u0"]).to(dev),
     }
+    if n_elp:
+        inp["elp"] = torch.from_numpy(batch["elp"]).to(dev)
+        inp["ne"] = torch.from_numpy(batch["ne"].astype(np.int32)).to(dev)
     out = {
         "u": torch.empty((B, n), dtype=torch.float64, device=dev),
         "foot": torch.empty((B, 3), dtype=torch.float64, device=dev),
@@ -148,11 +182,13 @@ def main():
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     status = out["status"].cpu().numpy()
     iters = out["iters"].cpu().numpy()
-    total_solves = world * B * K
+    B_total = B * world if (preset["per_gpu"] or args.batch is not None) else preset["batch"]
+    total_solves = B_total * K
     value = total_solves / elapsed
     # roofline of the dominant kernel (solve_kernel): algorithmic FP64 flops per launch / launch time
-    kname, m = solve_kernel_name(N, solver.rps, variant == alipmpc.VARIANT_MODI)
-    fpi = flops_per_iter(n, m, N, args.obstacles)
+    kname, m = solve_kernel_name(N, solver.rps, variant == alipmpc.VARIANT_MODI, fp32)
+    fpi = flops_per_iter(n, m, N, n_cir + n_elp)
+    peak = FP32_PEAK_TFLOPS if fp32 else FP64_PEAK_TFLOPS
     launch_flops = fpi * float(iters.sum())
     achieved = launch_flops / (kernel_ms * 1e-3) / 1e12
     traffic = None
@@ -161,18 +197,20 @@ def main():
         try:
             with open(tp) as fh:
                 tj = json.load(fh)
-            if tj.get("B") == B and tj.get("N") == N:
+            if tj.get("B") == B and tj.get("N") == N and not fp32 and not n_elp:
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
 
-    sweep = jacobian_sweep(alipmpc, scenes, cfg, args, dev) if (rank == 0 and args.sweep_batch > 0) else None
+    feas = feasible_fraction(alipmpc, solver, cfg, inp, out, dev, world, dist) if fp32 else None
+
+    sweep = jacobian_sweep(alipmpc, scenes, variant, args, dev) if (rank == 0 and args.sweep_batch > 0) else None
 
     cpu = cpu_mt = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(cfg, batch, args.cpu_seconds)
+        cpu = cpu_baseline(cfg, batch, args.cpu_seconds, workload=args.config)
         # the same C restatement with OpenMP over the host cores this job may use
-        cpu_mt = cpu_baseline(cfg, batch, args.cpu_seconds / 2, threads=args.cpu_threads)
+        cpu_mt = cpu_baseline(cfg, batch, args.cpu_seconds / 2, threads=args.cpu_threads, workload=args.config)
 
     if rank == 0:
         line = {
@@ -184,15 +222,16 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / K * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if preset["per_gpu"] or args.batch is not None else "strong",
             "vs_baseline": None,
-            "dtype": "f64",
+            "dtype": "f32" if fp32 else "f64",
             "data": "synthetic (rand_obs distribution, SURVEY 8d), generated per rank from (seed, rank)",
             "config": {
-                "workload": f"cfg2: B={B} ALIP initial states per GPU, N={N} horizon, {args.obstacles} circles, "
-                            f"variant={args.variant}, fp64, interior point (tol 1e-8, max_iter {cfg.max_iter} = the "
-                            f"reference's IPOPT cap)",
-                "batch_per_gpu": B, "global_batch": B * world, "horizon": N, "obstacles": args.obstacles,
+                "workload": f"{args.config}: {B_total} ALIP initial states ({B} on rank 0), N={N} horizon, "
+                            f"{n_cir} circles + {n_elp} ellipses, variant={args.variant}, "
+                            f"{'fp32' if fp32 else 'fp64'}, interior point (tol {cfg.tol:g}, max_iter {cfg.max_iter} "
+                            f"= the reference's IPOPT cap)",
+                "batch_per_gpu": B, "global_batch": B_total, "horizon": N, "obstacles": n_cir + n_elp,
                 "variant": args.variant, "parallelism": f"shard{world}" if world > 1 else "single",
                 "mean_iters": float(iters.mean()), "max_iters": int(iters.max()),
                 "status_counts": {str(k): int(v) for k, v in zip(*np.unique(status, return_counts=True))},
@@ -201,9 +240,9 @@ def main():
                 "kernel": kname,
                 "bound": "mfma",
                 "achieved": achieved,
-                "peak": FP64_PEAK_TFLOPS,
+                "peak": peak,
                 "unit": "TFLOP/s",
-                "frac": achieved / FP64_PEAK_TFLOPS,
+                "frac": achieved / peak,
                 "traffic": traffic,
                 "kernel_ms": kernel_ms,
                 "flops_per_iter": fpi,
@@ -212,20 +251,23 @@ def main():
             "cpu_baseline": cpu,
             "cpu_baseline_allcores": cpu_mt,
             "jacobian_sweep": sweep,
+            "feasible": feas,
         }
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()
 
 
-def jacobian_sweep(alipmpc, scenes, cfg, args, dev, reps=10):
+def jacobian_sweep(alipmpc, scenes, variant, args, dev, reps=10):
     """HBM roofline of the unfused Jacobian sweep (eval_kernel: f, grad f, c, J of the
-    reference callbacks at given u).  Algorithmic bytes per instance = 8(n + 8 + 3 n_c + 5 n_e) read +
-    8(1 + n + m + m n) written (n = 5N, m = padded rows)."""
+    reference callbacks at given u) on cfg2-shaped instances (N = 3, 5 circles) whatever --config is.
+    Algorithmic bytes per instance = 8(n + 8 + 3 n_c + 5 n_e) read + 8(1 + n + m + m n) written (n = 5N,
+    m = padded rows)."""
     import torch
+    cfg = alipmpc.default_cfg(variant, 3, nc_max=5, ne_max=0)
     Bs = args.sweep_batch
     s = alipmpc.Solver(cfg, device=dev.index)
-    bt = scenes.make_batch(Bs, seed=args.seed * 1000 + 7, n_cir=cfg.nc_max, N=cfg.N, scenes_per_batch=4096)
+    bt = scenes.make_batch_vec(Bs, seed=args.seed * 1000 + 7, n_cir=cfg.nc_max, N=cfg.N, fields=4096)
     n, m = 5 * cfg.N, cfg.N * s.rps
     inp = {"x0": torch.from_numpy(bt["x0"]).to(dev), "goal": torch.from_numpy(bt["goal"]).to(dev),
            "leg": torch.from_numpy(bt["leg"].astype(np.int8)).to(dev), "cir": torch.from_numpy(bt["cir"]).to(dev),
@@ -254,13 +296,48 @@ def jacobian_sweep(alipmpc, scenes, cfg, args, dev, reps=10):
             "evals_per_s": Bs / (ms * 1e-3)}
 
 
-def cpu_baseline(cfg, batch, seconds, threads=1):
-    """C restatement (oracle/liboracle.so) of the same algorithm, bounded sample of the same workload,
-    timed on this host (1 thread, or OpenMP over `threads`)."""
+def feasible_fraction(alipmpc, solver, cfg, inp, out, dev, world, dist, chunk=65536):
+    """cfg5: share of instances whose solution u, evaluated by the fp64 eval kernel (the reference
+    callbacks), violates no active constraint row by more than 1e-4 (the reference analogue is
+    status != 2, 86.6 % in its logs).  Also the share with status 0 or 1.  Counts are summed over ranks."""
+    import torch
+    c64 = alipmpc.default_cfg(cfg.variant, cfg.N, nc_max=cfg.nc_max, ne_max=cfg.ne_max)
+    ev = alipmpc.Solver(c64, device=dev.index)
+    B = inp["x0"].shape[0]
+    m = ev.m_max
+    feas = 0
+    for i0 in range(0, B, chunk):
+        i1 = min(B, i0 + chunk)
+        sub = {k: v[i0:i1] for k, v in inp.items() if k != "u0"}
+        sub["u"] = out["u"][i0:i1]
+        o = {"c": torch.empty((i1 - i0, m), dtype=torch.float64, device=dev),
+             "cl": torch.empty((i1 - i0, m), dtype=torch.float64, device=dev),
+             "cu": torch.empty((i1 - i0, m), dtype=torch.float64, device=dev),
+             "row_active": torch.empty((i1 - i0, m), dtype=torch.int8, device=dev)}
+        ev.eval_device(sub, o)
+        v = torch.clamp(torch.maximum(o["cl"] - o["c"], o["c"] - o["cu"]), min=0.0)
+        v = torch.where(o["row_active"] != 0, v, torch.zeros_like(v))
+        feas += int((v.amax(dim=1) <= 1e-4).sum().item())
+    st = out["status"]
+    conv = int(((st == 0) | (st == 1)).sum().item())
+    cnt = torch.tensor([feas, conv, B], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(cnt)
+    feas, conv, tot = (float(x) for x in cnt.tolist())
+    return {"feasible_fraction": feas / tot, "converged_fraction": conv / tot, "instances": int(tot),
+            "check": "fp64 reference callbacks at the fp32 solution, max active-row violation <= 1e-4"}
+
+
+def cpu_baseline(cfg, batch, seconds, threads=1, workload="cfg2"):
+    """C restatement (oracle/liboracle.so) of the same algorithm (fp64), bounded sample of the same
+    workload, timed on this host (1 thread, or OpenMP over `threads`)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as C
-    co = C.default_cfg(cfg.variant, cfg.N, nc_max=cfg.nc_max, ne_max=0)
+    co = C.default_cfg(cfg.variant, cfg.N, nc_max=cfg.nc_max, ne_max=cfg.ne_max)
     B = batch["x0"].shape[0]
+    ne_max = cfg.ne_max
+    elp = batch["elp"] if ne_max else None
+    ne = batch["ne"] if ne_max else None
     done = 0
     t0 = time.perf_counter()
     chunk = 64 * threads
@@ -268,12 +345,13 @@ def cpu_baseline(cfg, batch, seconds, threads=1):
         i0 = done % B
         i1 = min(i0 + chunk, B)
         C.solve_batch(co, batch["x0"][i0:i1], batch["goal"][i0:i1], batch["leg"][i0:i1], batch["cir"][i0:i1],
-                      batch["nc"][i0:i1], np.zeros((i1 - i0, 0, 5)), np.zeros(i1 - i0), batch["u0"][i0:i1],
+                      batch["nc"][i0:i1], elp[i0:i1] if ne_max else np.zeros((i1 - i0, 0, 5)),
+                      ne[i0:i1] if ne_max else np.zeros(i1 - i0), batch["u0"][i0:i1],
                       nthreads=threads)
         done += i1 - i0
     dt = time.perf_counter() - t0
     return {"value": done / dt, "unit": "solves/s", "cores": threads, "kind": "port",
-            "sample": f"{done} instances of the cfg2 workload (first {min(done, B)} of the GPU batch, cycled), "
+            "sample": f"{done} instances of the {workload} workload (first {min(done, B)} of the GPU batch, cycled), "
                       f"C oracle oracle/alipmpc_oracle.c, same interior-point algorithm, {threads} thread(s), "
                       f"{dt:.1f} s"}
 

@@ -5,7 +5,8 @@
   planner      MPCCBF drop-in (reference MPC_LIP_modi.MPCCBF signatures) + solve_batch
 """
 from ._lib import (Cfg, Solver, default_cfg, load, lib_path, num_vars, rows_per_step, EXPORTS, STATUS_NAMES,
-                   VARIANT_MODI, VARIANT_SIG_STEP, VARIANT_DD, PREC_FP64, PREC_FP32, ROLLOUT_DONE)
+                   VARIANT_MODI, VARIANT_SIG_STEP, VARIANT_DD, PREC_FP64, PREC_FP32, ROLLOUT_DONE, FP32_TOL,
+                   FP32_ACCEPTABLE_TOL)
 
 __all__ = ["Cfg", "Solver", "default_cfg", "load", "lib_path", "num_vars", "rows_per_step", "EXPORTS",
-           "STATUS_NAMES", "VARIANT_MODI", "VARIANT_SIG_STEP", "VARIANT_DD", "PREC_FP64", "PREC_FP32", "ROLLOUT_DONE"]
+           "STATUS_NAMES", "VARIANT_MODI", "VARIANT_SIG_STEP", "VARIANT_DD", "PREC_FP64", "PREC_FP32", "ROLLOUT_DONE", "FP32_TOL", "FP32_ACCEPTABLE_TOL"]

@@ -83,11 +83,21 @@ def load(build_if_missing=True):
     return L
 
 
+# fp32 solve kernels (cfg.precision = PREC_FP32, BASELINE cfg5): the fp64 tolerance 1e-8 is below fp32
+# resolution, so unless the caller sets them the fp32 tolerances are tol 1e-4 / acceptable 1e-3 (tools/
+# fp32_study.py: foothold within 1e-3 of the fp64 solve on 99.9 % of the instances both converge on, the
+# same feasible fraction, 1.5x the fp64 throughput).
+FP32_TOL, FP32_ACCEPTABLE_TOL = 1e-4, 1e-3
+
+
 def default_cfg(variant=VARIANT_MODI, N=3, **overrides):
     c = Cfg()
     rc = load().alipmpc_default_cfg(variant, N, ctypes.byref(c))
     if rc != 0:
         raise ValueError(f"alipmpc_default_cfg({variant}, {N}) -> {rc}")
+    if overrides.get("precision") == PREC_FP32:
+        overrides.setdefault("tol", FP32_TOL)
+        overrides.setdefault("acceptable_tol", FP32_ACCEPTABLE_TOL)
     for k, v in overrides.items():
         if not hasattr(c, k):
             raise AttributeError(k)

@@ -1,10 +1,16 @@
 """Build libalipmpc.so (HIP kernels + C ABI) in-tree for gfx950 with hipcc.
 
 The library is the product: there is no CPU execution path behind it.
+
+csrc/alipmpc.hip is compiled as 7 translation units in parallel — ALIP_PART=0 (host code, C ABI, rollout
+kernels) and ALIP_PART=1..6 (the solve/eval kernels of one horizon N each, fp64 and fp32) — and linked into
+one shared library.  `ALIPMPC_SINGLE_TU=1` builds it as one TU instead (slower, same code).
 """
 import os
 import subprocess
 import sys
+import tempfile
+from concurrent.futures import ThreadPoolExecutor
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)                         # mujoco-lip-mpc-simulation_amd/
@@ -12,9 +18,11 @@ REPO = os.path.dirname(ROOT)
 SRC = os.path.join(ROOT, "csrc", "alipmpc.hip")
 HDR = os.path.join(REPO, "include", "alipmpc.h")
 LIB = os.path.join(PKG, "libalipmpc.so")
+PARTS = range(0, 7)
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+ARCH = ["--offload-arch=gfx950"]
+FLAGS = ["-O3", "-std=c++17", "-fPIC",
          # keep MachineLICM from hoisting f64 literals / LDS addresses out of the interior-point loop
          # (it pins ~100 VGPRs across the whole solve and forces spills)
          "-mllvm", "-disable-machine-licm",
@@ -28,14 +36,29 @@ def needs_build():
     return any(os.path.getmtime(p) > t for p in (SRC, HDR, __file__))
 
 
-def build(force=False, verbose=True):
-    if not force and not needs_build():
-        return LIB
-    cmd = [HIPCC, *FLAGS, "-o", LIB + ".tmp", SRC]
+def _run(cmd, verbose):
     if verbose:
         print("[alipmpc] " + " ".join(cmd), file=sys.stderr)
     subprocess.check_call(cmd)
-    os.replace(LIB + ".tmp", LIB)
+
+
+def build(force=False, verbose=True, extra=()):
+    if not force and not needs_build():
+        return LIB
+    tmp_lib = LIB + ".tmp"
+    if os.environ.get("ALIPMPC_SINGLE_TU") == "1":
+        _run([HIPCC, *ARCH, *FLAGS, *extra, "-shared", "-o", tmp_lib, SRC], verbose)
+    else:
+        jobs = max(1, min(len(PARTS), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1))))
+        with tempfile.TemporaryDirectory(prefix="alipmpc_build_") as td:
+            objs = [os.path.join(td, f"part{k}.o") for k in PARTS]
+            cmds = [[HIPCC, *ARCH, *FLAGS, *extra, f"-DALIP_PART={k}", "-c", "-o", o, SRC]
+                    for k, o in zip(PARTS, objs)]
+            with ThreadPoolExecutor(jobs) as ex:
+                for f in [ex.submit(_run, c, verbose) for c in cmds]:
+                    f.result()
+            _run([HIPCC, *ARCH, "-shared", "-fPIC", "-o", tmp_lib, *objs], verbose)
+    os.replace(tmp_lib, LIB)
     return LIB
 
 

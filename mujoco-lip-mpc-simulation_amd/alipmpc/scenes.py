@@ -116,3 +116,92 @@ def make_batch(B, seed=0, n_cir=5, n_elp=0, N=3, nc_max=None, ne_max=None, scene
     goal = np.tile(np.array(GOAL), (B, 1))
     return dict(x0=x0, goal=goal, leg=leg, cir=cir, nc=nc, elp=elp if ne_max else None, ne=ne if ne_max else None,
                 u0=u0)
+
+
+def make_batch_vec(B, seed=0, n_cir=5, n_elp=0, N=3, fields=None, max_rounds=4000):
+    """Same distribution as make_batch, vectorised over instances, with `fields` distinct obstacle fields
+    (default: one PER INSTANCE — the Monte-Carlo sweep of BASELINE cfg5, 1M randomized scenes; instance b
+    uses field b % fields).  Every round draws candidates for each unfinished field and accepts the first
+    one that passes the same spacing rule (halved after 2000 consecutive rejections, as random_circles);
+    initial states are rejection-sampled per instance the same way.  Not stream-identical to make_batch
+    (different draw order), distribution-identical."""
+    rng = np.random.default_rng(seed)
+    tot = n_cir + n_elp
+    K = tot + 2
+    F = B if fields is None else max(1, min(int(fields), B))
+    B_inst, B = B, F
+    obs = np.zeros((B, K, 3))
+    obs[:, 0] = (10.0, 10.0, 0.3)
+    obs[:, 1] = (0.0, 0.0, 1.0)
+    cnt = np.full(B, 2)
+    spacing = np.full(B, 0.8)
+    tries = np.zeros(B, np.int64)
+    C = 32   # candidates per field and round; the first acceptable one is taken (= sequential rejection)
+    for _ in range(max_rounds * max(tot, 1)):
+        todo = np.nonzero(cnt < K)[0]
+        if todo.size == 0:
+            break
+        x = np.round(8.5 * rng.random((todo.size, C)), 2)
+        y = np.round(8.5 * rng.random((todo.size, C)), 2)
+        r = np.round(0.65 * rng.random((todo.size, C)) + 0.35, 2)
+        o = obs[todo]
+        slot = np.arange(K)[None, None, :] < cnt[todo, None, None]
+        d = (x[:, :, None] - o[:, None, :, 0]) ** 2 + (y[:, :, None] - o[:, None, :, 1]) ** 2 - \
+            (r[:, :, None] + o[:, None, :, 2] + 2 * spacing[todo, None, None]) ** 2
+        okc = np.all((d >= 0) | ~slot, axis=2)                  # (todo, C)
+        first = np.argmax(okc, axis=1)
+        anyok = okc[np.arange(todo.size), first]
+        # the 2000-rejection relaxation applies within the candidate sequence too
+        nrej = np.where(anyok, first, C)
+        over = tries[todo] + nrej > 2000
+        ok = anyok & ~over
+        acc = todo[ok]
+        obs[acc, cnt[acc]] = np.stack([x[ok, first[ok]], y[ok, first[ok]], r[ok, first[ok]]], axis=1)
+        cnt[acc] += 1
+        tries[acc] = 0
+        rej = todo[~ok]
+        tries[rej] += np.minimum(nrej[~ok], 2001 - tries[rej])
+        relax = rej[tries[rej] > 2000]
+        spacing[relax] *= 0.5
+        tries[relax] = 0
+    assert np.all(cnt == K), "obstacle placement did not finish"
+    obs = obs[:, 2:]
+    if n_elp > 0:   # to_mix: every second obstacle becomes an ellipse
+        ci = np.arange(0, tot, 2)
+        ei = np.arange(1, tot, 2)
+        cir = obs[:, ci]
+        a = obs[:, ei, 2]
+        b = np.round((a / 2) * rng.random(a.shape) + a / 2, 2)
+        phi = np.round(rng.integers(0, 181, a.shape) * np.pi / 180, 2)
+        elp = np.concatenate([obs[:, ei, :2], a[..., None], b[..., None], phi[..., None]], axis=2)
+        elp = elp + np.array([0, 0, SAFE_DIS, SAFE_DIS, 0])
+    else:
+        cir, elp = obs, np.zeros((B, 0, 5))
+    cir = cir + np.array([0, 0, SAFE_DIS])
+    if B_inst != F:   # instance b -> field b % F
+        idx = np.arange(B_inst) % F
+        cir, elp, B = cir[idx], elp[idx], B_inst
+    # initial states outside every inflated obstacle (+0.2) and > 0.5 from the goal
+    pos = np.zeros((B, 2))
+    todo = np.arange(B)
+    while todo.size:
+        p = rng.uniform(0.0, 10.0, (todo.size, 2))
+        ok = np.hypot(p[:, 0] - GOAL[0], p[:, 1] - GOAL[1]) > 0.5
+        ok &= np.all(np.hypot(p[:, None, 0] - cir[todo, :, 0], p[:, None, 1] - cir[todo, :, 1]) >=
+                     cir[todo, :, 2] + 0.2, axis=1)
+        if elp.shape[1]:
+            ok &= np.all(np.hypot(p[:, None, 0] - elp[todo, :, 0], p[:, None, 1] - elp[todo, :, 1]) >=
+                         np.maximum(elp[todo, :, 2], elp[todo, :, 3]) + 0.2, axis=1)
+        pos[todo[ok]] = p[ok]
+        todo = todo[~ok]
+    leg = rng.choice(np.array([-1, 1], np.int8), B)
+    th = np.arctan2(GOAL[1] - pos[:, 1], GOAL[0] - pos[:, 0]) + rng.normal(0.0, 0.2, B)
+    vbx = rng.uniform(0.45, 0.75, B)
+    vby = -leg * rng.uniform(0.17, 0.33, B)
+    c, s = np.cos(th), np.sin(th)
+    x0 = np.stack([pos[:, 0], pos[:, 1], c * vbx - s * vby, s * vbx + c * vby, th], axis=1)
+    return dict(x0=x0, goal=np.tile(np.array(GOAL), (B, 1)), leg=leg,
+                cir=np.ascontiguousarray(cir), nc=np.full(B, cir.shape[1], np.int32),
+                elp=np.ascontiguousarray(elp) if n_elp else None,
+                ne=np.full(B, elp.shape[1], np.int32) if n_elp else None,
+                u0=np.tile(x0, (1, N)))

@@ -36,6 +36,15 @@
 
 #include "../../include/alipmpc.h"
 
+// Build partitioning (see the kernel launchers below): ALIP_PART = 0 host code, 1..6 one horizon each.
+#ifndef ALIP_PART
+#define ALIP_PART_HOST 1
+#define ALIP_PART_N(k) 1
+#else
+#define ALIP_PART_HOST (ALIP_PART == 0)
+#define ALIP_PART_N(k) (ALIP_PART == (k))
+#endif
+
 namespace alip {
 
 constexpr int WAVE = 64;
@@ -185,55 +194,142 @@ __device__ __forceinline__ void swap32(double v, double& a, double& b)
     b = __hiloint2double((int)hi[1], (int)lo[1]);
 }
 
+// fp32 counterparts (the solve kernel is templated on its arithmetic type R, cfg.precision)
+__device__ __forceinline__ float uni(float v)
+{
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+__device__ __forceinline__ float bcast(float v, int src)
+{
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), src));
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v)
+{
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ void swap16(float v, float& a, float& b)
+{
+    auto x = __builtin_amdgcn_permlane16_swap((unsigned)__float_as_int(v), (unsigned)__float_as_int(v), false, false);
+    a = __int_as_float((int)x[0]);
+    b = __int_as_float((int)x[1]);
+}
+__device__ __forceinline__ void swap32(float v, float& a, float& b)
+{
+    auto x = __builtin_amdgcn_permlane32_swap((unsigned)__float_as_int(v), (unsigned)__float_as_int(v), false, false);
+    a = __int_as_float((int)x[0]);
+    b = __int_as_float((int)x[1]);
+}
+
 struct OpAdd {
-    __device__ double operator()(double a, double b) const { return a + b; }
+    template <class T>
+    __device__ T operator()(T a, T b) const { return a + b; }
 };
 struct OpMax {
-    __device__ double operator()(double a, double b) const { return fmax(a, b); }
+    template <class T>
+    __device__ T operator()(T a, T b) const { return fmax(a, b); }
 };
 struct OpMin {
-    __device__ double operator()(double a, double b) const { return fmin(a, b); }
+    template <class T>
+    __device__ T operator()(T a, T b) const { return fmin(a, b); }
 };
 
 // butterfly over all 64 lanes; every lane receives the result.
 //   quad_perm [1,0,3,2] (l^1), quad_perm [2,3,0,1] (l^2), row_half_mirror (quads of a half-row),
 //   row_mirror (half-rows), permlane16_swap (l^16), permlane32_swap (l^32)
-template <class Op>
-__device__ __forceinline__ double wreduce(double v, Op op)
+template <class T, class Op>
+__device__ __forceinline__ T wreduce(T v, Op op)
 {
     v = op(v, dpp<0xB1>(v));
     v = op(v, dpp<0x4E>(v));
     v = op(v, dpp<0x141>(v));
     v = op(v, dpp<0x140>(v));
-    double a, b;
+    T a, b;
     swap16(v, a, b);
     v = op(a, b);
     swap32(v, a, b);
     return uni(op(a, b));
 }
-__device__ __forceinline__ double wsum(double v) { return wreduce(v, OpAdd()); }
-__device__ __forceinline__ double wmax(double v) { return wreduce(v, OpMax()); }
-__device__ __forceinline__ double wmin(double v) { return wreduce(v, OpMin()); }
-__device__ __forceinline__ void wsum2(double& a, double& b)
+template <class T>
+__device__ __forceinline__ T wsum(T v) { return wreduce(v, OpAdd()); }
+template <class T>
+__device__ __forceinline__ T wmax(T v) { return wreduce(v, OpMax()); }
+template <class T>
+__device__ __forceinline__ T wmin(T v) { return wreduce(v, OpMin()); }
+template <class T>
+__device__ __forceinline__ void wsum2(T& a, T& b)
 {
     a = wsum(a);
     b = wsum(b);
 }
 // sum over the 4 lane groups (lanes c, c+16, c+32, c+48)
-__device__ __forceinline__ double gsum(double v)
+template <class T>
+__device__ __forceinline__ T gsum(T v)
 {
-    double a, b;
+    T a, b;
     swap16(v, a, b);
     v = a + b;
     swap32(v, a, b);
     return a + b;
 }
 
+// ---- type-generic scalar pieces of the solve kernel (R = double | float)
+__device__ __forceinline__ void msincos(double x, double* s, double* c) { sincos(x, s, c); }
+__device__ __forceinline__ void msincos(float x, float* s, float* c) { sincosf(x, s, c); }
+
+// 4 consecutive LDS values (16-byte aligned) as b128 accesses
+__device__ __forceinline__ void ld4(const double* p, double& a, double& b, double& c, double& d)
+{
+    const double2* q = reinterpret_cast<const double2*>(p);
+    const double2 x = q[0], y = q[1];
+    a = x.x; b = x.y; c = y.x; d = y.y;
+}
+__device__ __forceinline__ void ld4(const float* p, float& a, float& b, float& c, float& d)
+{
+    const float4 x = *reinterpret_cast<const float4*>(p);
+    a = x.x; b = x.y; c = x.z; d = x.w;
+}
+__device__ __forceinline__ void st4(double* p, double a, double b, double c, double d)
+{
+    double2* q = reinterpret_cast<double2*>(p);
+    q[0] = make_double2(a, b);
+    q[1] = make_double2(c, d);
+}
+__device__ __forceinline__ void st4(float* p, float a, float b, float c, float d)
+{
+    *reinterpret_cast<float4*>(p) = make_float4(a, b, c, d);
+}
+
+// 16x16x4 MFMA with one operand element per lane (A[l&15][l>>4], B[l>>4][l&15]).  C/D layout: f64
+// row = (l>>4) + 4 i, f32 row = 4 (l>>4) + i (cdna_hip_programming.md §3), col = l & 15.
+typedef float f4 __attribute__((ext_vector_type(4)));
+template <class R>
+struct Mfma;
+template <>
+struct Mfma<double> {
+    typedef d4 acc;
+    __device__ static __forceinline__ d4 run(double a, double b, d4 c)
+    {
+        return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+    }
+    __device__ static __forceinline__ int row(int g4, int i) { return g4 + 4 * i; }
+};
+template <>
+struct Mfma<float> {
+    typedef f4 acc;
+    __device__ static __forceinline__ f4 run(float a, float b, f4 c)
+    {
+        return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+    }
+    __device__ static __forceinline__ int row(int g4, int i) { return 4 * g4 + i; }
+};
+
 // ------------------------------------------------------------------------------------------------
 // per-wave LDS workspace
 // ------------------------------------------------------------------------------------------------
 template <int N>
 struct WS {
+    typedef double real;
     double* V;      // NG  current generator values
     double* Vt;     // NG  trial values
     double* dV;     // NG  step
@@ -328,8 +424,8 @@ __device__ __forceinline__ RowInfo decode_row(const KP& P, int r, int nc_sel, in
 // split (solve layout, modi): f_en = vbx + s|dth| in [bvx_lo, bvx_hi] becomes vbx +- s dth <= bvx_hi — the
 // same feasible set (|x| <= c <=> +-x <= c; the lower bound is implied by the vbx row since s > 0), but
 // smooth, so Newton steps are not trapped at the kink dth = 0.
-__device__ __forceinline__ void row_bounds(const KP& P, const RowInfo& ri, int leg, double& cl, double& cu,
-                                           bool split = false)
+template <class R>
+__device__ __forceinline__ void row_bounds(const KP& P, const RowInfo& ri, int leg, R& cl, R& cu, bool split = false)
 {
     switch (ri.type) {
     case R_VBX:
@@ -349,15 +445,15 @@ __device__ __forceinline__ void row_bounds(const KP& P, const RowInfo& ri, int l
     }
     case R_CIR:
     case R_ELP:
-        cl = 0.0;
+        cl = R(0);
         cu = INFINITY;
         break;
     case R_LEG:
-        cl = 0.0;
+        cl = R(0);
         cu = P.leg2;
         break;
     case R_DTH:
-        cl = -P.dth;
+        cl = R(-P.dth);
         cu = P.dth;
         break;
     default:
@@ -517,11 +613,13 @@ __device__ __forceinline__ double jrow_col(const double* rcoef, const uint8_t* r
 }
 
 // ------------------------------------------------------------------------------------------------
-// instance prologue: load inputs, select_obs, detour goal, ellipse forms, V = E x0 + G u0
+// instance prologue: load inputs, select_obs, detour goal, ellipse forms, V = E x0 + G u0.
+// Computed in fp64 for either workspace type (the discrete select/detour decisions do not depend on
+// cfg.precision); results are stored into the workspace's type.
 // ------------------------------------------------------------------------------------------------
 template <int N, bool FROM_U, class WT>
-__device__ void prologue(const KP& P, const WT& w, const double* G, const double* E, long long b, double& gxg,
-                         double& gyg, int& legv, double& uj)
+__device__ void prologue(const KP& P, const WT& w, const typename WT::real* G, const typename WT::real* E,
+                         long long b, double& gxg, double& gyg, int& legv, double& uj)
 {
     using D = Dim<N>;
     const int lane = lane_id();
@@ -563,11 +661,11 @@ __device__ void prologue(const KP& P, const WT& w, const double* G, const double
         unsigned long long m = __ballot(keep);
         int pos = __builtin_popcountll(m & ((1ull << lane) - 1ull));
         if (keep) {
-            double* o = w.obs + 3 * P.nc_max + 5 * pos;
+            auto* o = w.obs + 3 * P.nc_max + 5 * pos;
             for (int i = 0; i < 5; ++i) o[i] = e[i];
             double ce, se;
             sincos(e[4], &se, &ce);
-            double* qq = w.obs + 3 * P.nc_max + 5 * P.ne_max;
+            auto* qq = w.obs + 3 * P.nc_max + 5 * P.ne_max;
             qq[pos] = (e[3] * ce) * (e[3] * ce) + (e[2] * se) * (e[2] * se);
             qq[P.ne_max + pos] = 2 * ce * se * (e[3] * e[3] - e[2] * e[2]);
             qq[2 * P.ne_max + pos] = (e[3] * se) * (e[3] * se) + (e[2] * ce) * (e[2] * ce);
@@ -586,7 +684,7 @@ __device__ void prologue(const KP& P, const WT& w, const double* G, const double
         bool fire = false;
         double nx = 0, ny = 0;
         if (lane < ncs) {
-            const double* c = w.obs + 3 * lane;
+            const auto* c = w.obs + 3 * lane;
             double cen = (x0v0 - c[0]) * (x0v0 - c[0]) + (x0v1 - c[1]) * (x0v1 - c[1]);
             double gd = (x0v0 - g0) * (x0v0 - g0) + (x0v1 - g1) * (x0v1 - g1);
             if (cen < gd && cen < 9 * c[2] * c[2]) {
@@ -631,7 +729,7 @@ __device__ void prologue(const KP& P, const WT& w, const double* G, const double
             double v = 0.0;
 #pragma unroll
             for (int c = 0; c < 5; ++c) v += E[t * 5 + c] * xb[c];
-            const double* gr = G + t * D::NCPU;
+            const auto* gr = G + t * D::NCPU;
 #pragma unroll
             for (int j = 0; j < nu; ++j) v += gr[j] * w.Vt[j];
             w.V[t] = v;
@@ -656,7 +754,7 @@ __device__ void prologue(const KP& P, const WT& w, const double* G, const double
         double v = 0.0;
 #pragma unroll
         for (int c = 0; c < 5; ++c) v += E[t * 5 + c] * xb[c];
-        const double* gr = G + t * D::NCP;
+        const auto* gr = G + t * D::NCP;
 #pragma unroll
         for (int j = 0; j < D::n; ++j) v += gr[j] * w.Vt[j];
         w.V[t] = v;
@@ -682,22 +780,33 @@ __device__ __forceinline__ double rcp_nr(double x)
     e = fma(-x, y, 1.0);
     return fma(y, e, y);
 }
+// fp32: the hardware estimates are ~1 ulp already; one Newton step makes them correctly rounded-ish
+__device__ __forceinline__ float rsqrt_nr(float d)
+{
+    float y = __builtin_amdgcn_rsqf(d);
+    return y * fmaf(-0.5f * d * y, y, 1.5f);
+}
+__device__ __forceinline__ float rcp_nr(float x)
+{
+    float y = __builtin_amdgcn_rcpf(x);
+    return fmaf(y, fmaf(-x, y, 1.0f), y);
+}
 
 // ------------------------------------------------------------------------------------------------
 // register Cholesky: lane i (< n) holds row i of the (regularised) KKT matrix in a[0..n-1].
 // Right-looking; column j is broadcast with readlane (uniform lane index, compile-time register).
 // On success lane i holds row i of L in a[0..i] and idg[j] = 1 / L[j][j] (uniform).
 // ------------------------------------------------------------------------------------------------
-template <int n>
-__device__ __forceinline__ bool chol_rows(double (&a)[n], double& myidg, int lane)
+template <int n, class R>
+__device__ __forceinline__ bool chol_rows(R (&a)[n], R& myidg, int lane)
 {
 #pragma unroll
     for (int j = 0; j < n; ++j) {
-        const double d = bcast(a[j], j);
-        if (!(d > 0.0)) return false;   // wave-uniform
-        const double inv = rsqrt_nr(d);
+        const R d = bcast(a[j], j);
+        if (!(d > R(0))) return false;   // wave-uniform
+        const R inv = rsqrt_nr(d);
         myidg = lane == j ? inv : myidg;
-        const double lij = a[j] * inv;
+        const R lij = a[j] * inv;
         a[j] = lane == j ? d * inv : lij;
 #pragma unroll
         for (int k = j + 1; k < n; ++k) a[k] -= lij * bcast(lij, k);
@@ -711,43 +820,45 @@ __device__ __forceinline__ bool chol_rows(double (&a)[n], double& myidg, int lan
 // grad f and J^T y come out of ONE J-layout sweep, and grad f . dV out of the row-layout dS pass.
 // mo4 = mr4 + 4 ceil(N/4) rows in total.
 // ------------------------------------------------------------------------------------------------
-template <int N>
+template <int N, class R>
 struct WSS {
-    double* V;      // NG   current generator values (canonical copy; rows keep register copies)
-    double* Vt;     // NG   prologue scratch
-    double* dV;     // NG   step
-    double* CT;     // N+1  cos / sin of theta_k at V (written by the VBX rows, read by the Hessian lanes)
-    double* ST;     // N+1
-    double* S;      // (N+1) x 64 Hessian blocks
-    double* hobj;   // (N+1) x 6 objective Hessian parts (written by the OBJ rows)
-    double* rcoef;  // mo4 x 4
-    double* cst;    // 16 per-instance constants read at use (keeps long-lived uniforms out of registers)
-    double* ry;     // mo4   y (constraint rows), -1 (OBJ rows)
-    double* rsig;   // mo4   Sigma
-    double* rw;     // mo4   rhs weights (OBJ rows: -1)
-    double* obs;    // prologue layout: circles 3*nc_max, ellipses 5*ne_max, then qa, qb, qc, ek (4*ne_max)
-    double* obs6;   // (nc_max + ne_max) x 6 unified quadratic form [ox, oy, qa, qb, qc, ek] per row slot
-    double* K;      // NCP x KLD
-    double* rclo;   // mr4 original bounds (status / infeasibility checks only)
-    double* rcuo;   // mr4
+    typedef R real;
+    R* V;      // NG   current generator values (canonical copy; rows keep register copies)
+    R* Vt;     // NG   prologue scratch
+    R* dV;     // NG   step
+    R* CT;     // N+1  cos / sin of theta_k at V (written by the VBX rows, read by the Hessian lanes)
+    R* ST;     // N+1
+    R* S;      // (N+1) x 64 Hessian blocks
+    R* hobj;   // (N+1) x 6 objective Hessian parts (written by the OBJ rows)
+    R* rcoef;  // mo4 x 4
+    R* cst;    // 16 per-instance constants read at use (keeps long-lived uniforms out of registers)
+    R* ry;     // mo4   y (constraint rows), -1 (OBJ rows)
+    R* rsig;   // mo4   Sigma
+    R* rw;     // mo4   rhs weights (OBJ rows: -1)
+    R* obs;    // prologue layout: circles 3*nc_max, ellipses 5*ne_max, then qa, qb, qc, ek (4*ne_max)
+    R* obs6;   // (nc_max + ne_max) x 6 unified quadratic form [ox, oy, qa, qb, qc, ek] per row slot
+    R* K;      // NCP x KLD
+    R* rclo;   // mr4 original bounds (status / infeasibility checks only)
+    R* rcuo;   // mr4
     int* nsel;      // [0] = nc_sel, [1] = ne_sel
     uint32_t* rgen; // mo4 packed generator indices (4 x 8 bit)
 };
 
-template <int N>
-__host__ __device__ constexpr int wss_doubles(int nc_max, int ne_max, int mr4, int mo4)
+template <int N, class R>
+__host__ __device__ constexpr int wss_elems(int nc_max, int ne_max, int mr4, int mo4)
 {
     int d = 16 + 3 * Dim<N>::NG + 2 * (N + 1) + 64 * (N + 1) + 6 * (N + 1) + 4 * mo4 + 3 * mo4 + 3 * nc_max +
-            9 * ne_max + 6 * (nc_max + ne_max) + 6 + Dim<N>::NCP * Dim<N>::KLD + 2 * mr4 + 1 + (mo4 + 1) / 2;
-    return (d + 3) & ~3;   // 32-byte multiple: rcoef rows are read as 2 x b128
+            9 * ne_max + 6 * (nc_max + ne_max) + 6 + Dim<N>::NCP * Dim<N>::KLD + 2 * mr4 +
+            (int)(8 / sizeof(R)) + (int)((4 * mo4 + sizeof(R) - 1) / sizeof(R));
+    return (d + 3) & ~3;   // 4-element multiple: rcoef rows (4 x R) are read as b128 (double: 2 x b128)
 }
 
-template <int N>
-__device__ WSS<N> carve_s(double* base, int nc_max, int ne_max, int mr4, int mo4)
+template <int N, class R>
+__device__ WSS<N, R> carve_s(R* base, int nc_max, int ne_max, int mr4, int mo4)
 {
     using D = Dim<N>;
-    WSS<N> w;
-    double* p = base;
+    WSS<N, R> w;
+    R* p = base;
     w.rcoef = p; p += 4 * mo4;   // first: 32-byte aligned
     w.cst = p; p += 16;
     w.V = p; p += D::NG;
@@ -765,7 +876,7 @@ __device__ WSS<N> carve_s(double* base, int nc_max, int ne_max, int mr4, int mo4
     w.K = p; p += D::NCP * D::KLD;
     w.rclo = p; p += mr4;
     w.rcuo = p; p += mr4;
-    w.nsel = reinterpret_cast<int*>(p); p += 1;
+    w.nsel = reinterpret_cast<int*>(p); p += 8 / sizeof(R);
     w.rgen = reinterpret_cast<uint32_t*>(p);
     return w;
 }
@@ -806,50 +917,54 @@ __device__ __forceinline__ int gen_i(uint32_t pk, int i) { return (int)((pk >> (
 
 // the transcendental part of a row: VEL rows sincos(theta_{k+1}) -> (a0, a1) = (sin, cos);
 // OBJ rows phi = theta_k - atan2(goal - p) -> a0.  (Computed for every lane; lanes keep what they need.)
-__device__ __forceinline__ void row_trans(int type, const double (&v)[4], double gxg, double gyg, double& a0, double& a1)
+template <class R>
+__device__ __forceinline__ void row_trans(int type, const R (&v)[4], R gxg, R gyg, R& a0, R& a1)
 {
-    double s_, c_;
-    sincos(v[2], &s_, &c_);
-    const double at = atan2(gyg - v[1], gxg - v[0]);
+    R s_, c_;
+    msincos(v[2], &s_, &c_);
+    const R at = atan2(gyg - v[1], gxg - v[0]);
     a0 = type == R_OBJ ? v[2] - at : s_;
     a1 = c_;
 }
 
+template <class R>
 struct RowK {   // uniform constants of the row functions
-    double gm1, s, q, p, r, gxg, gyg;
+    R gm1, s, q, p, r, gxg, gyg;
 };
 // cst slots
 enum { K_GM1 = 0, K_S, K_Q, K_P, K_R, K_GXG, K_GYG, K_THMAX, K_THMIN, K_MACT, K_NBL, K_TOL, K_ACCTOL };
-__device__ __forceinline__ RowK load_rowk(const double* cst)
+template <class R>
+__device__ __forceinline__ RowK<R> load_rowk(const R* cst)
 {
-    RowK C;
+    RowK<R> C;
     C.gm1 = cst[K_GM1]; C.s = cst[K_S]; C.q = cst[K_Q]; C.p = cst[K_P]; C.r = cst[K_R];
     C.gxg = cst[K_GXG]; C.gyg = cst[K_GYG];
     return C;
 }
 
 // value of row `type` at generator values v (branch-free: every family is computed, one is selected)
-__device__ __forceinline__ double row_value(int type, int k, const double (&v)[4], double a0, double a1,
-                                            const double (&o)[6], const RowK& C)
+template <class R>
+__device__ __forceinline__ R row_value(int type, int k, const R (&v)[4], R a0, R a1,
+                                            const R (&o)[6], const RowK<R>& C)
 {
     // velocity family (f_en halves: vbx +- s dth)
     const bool vby = type == R_VBY;
-    const double ca = vby ? -a0 : a1, cb = vby ? a1 : a0;
-    const double sd = type == R_FEN ? C.s : (type == R_FENM ? -C.s : 0.0);
-    const double cvel = ca * v[0] + cb * v[1] + sd * v[3];
+    const R ca = vby ? -a0 : a1, cb = vby ? a1 : a0;
+    const R sd = type == R_FEN ? C.s : (type == R_FENM ? -C.s : R(0));
+    const R cvel = ca * v[0] + cb * v[1] + sd * v[3];
     // D-CBF (circle == ellipse with qa = qc = 1, qb = 0, ek = r^2)
-    const double x1 = v[0] - o[0], y1 = v[1] - o[1], x0 = v[2] - o[0], y0 = v[3] - o[1];
-    const double h1 = o[2] * x1 * x1 + o[3] * x1 * y1 + o[4] * y1 * y1 - o[5];
-    const double h0 = o[2] * x0 * x0 + o[3] * x0 * y0 + o[4] * y0 * y0 - o[5];
-    const double cobs = h1 + C.gm1 * h0;
+    const R x1 = v[0] - o[0], y1 = v[1] - o[1], x0 = v[2] - o[0], y0 = v[3] - o[1];
+    const R h1 = o[2] * x1 * x1 + o[3] * x1 * y1 + o[4] * y1 * y1 - o[5];
+    const R h0 = o[2] * x0 * x0 + o[3] * x0 * y0 + o[4] * y0 * y0 - o[5];
+    const R cobs = h1 + C.gm1 * h0;
     // leg length
-    const double ex = v[0] - v[2], ey = v[1] - v[3];
-    const double cleg = ex * ex + ey * ey;
+    const R ex = v[0] - v[2], ey = v[1] - v[3];
+    const R cleg = ex * ex + ey * ey;
     // objective term f_k
-    const double w = C.q + (k == 1 ? C.p : 0.0);
-    const double dxg = C.gxg - v[0], dyg = C.gyg - v[1];
-    const double cobj = w * (dxg * dxg + dyg * dyg) + C.r * a0 * a0;
-    double c = 0.0;
+    const R w = C.q + (k == 1 ? C.p : R(0));
+    const R dxg = C.gxg - v[0], dyg = C.gyg - v[1];
+    const R cobj = w * (dxg * dxg + dyg * dyg) + C.r * a0 * a0;
+    R c = R(0);
     c = (type == R_VBX || vby || type == R_FEN || type == R_FENM) ? cvel : c;
     c = (type == R_CIR || type == R_ELP) ? cobs : c;
     c = type == R_LEG ? cleg : c;
@@ -860,26 +975,27 @@ __device__ __forceinline__ double row_value(int type, int k, const double (&v)[4
 
 // generator-form gradient coefficients of row `type` (OBJ rows: grad f_k; hx = its 6 Hessian parts
 // [h00 h01 h11 h04 h14 h44] on (px, py, theta) of x_k)
-__device__ __forceinline__ void row_coef(int type, int k, const double (&v)[4], double a0, double a1,
-                                         const double (&o)[6], const RowK& C, double (&cf)[4], double (&hx)[6])
+template <class R>
+__device__ __forceinline__ void row_coef(int type, int k, const R (&v)[4], R a0, R a1,
+                                         const R (&o)[6], const RowK<R>& C, R (&cf)[4], R (&hx)[6])
 {
     const bool vby = type == R_VBY, vel = type == R_VBX || vby || type == R_FEN || type == R_FENM;
     const bool obs = type == R_CIR || type == R_ELP;
     // velocity family: d/dtheta of (ca, cb)
-    const double ca = vby ? -a0 : a1, cb = vby ? a1 : a0;
-    const double da = vby ? -a1 : -a0, db = vby ? -a0 : a1;
+    const R ca = vby ? -a0 : a1, cb = vby ? a1 : a0;
+    const R da = vby ? -a1 : -a0, db = vby ? -a0 : a1;
     // D-CBF
-    const double x1 = v[0] - o[0], y1 = v[1] - o[1], x0 = v[2] - o[0], y0 = v[3] - o[1];
+    const R x1 = v[0] - o[0], y1 = v[1] - o[1], x0 = v[2] - o[0], y0 = v[3] - o[1];
     // leg
-    const double ex = v[0] - v[2], ey = v[1] - v[3];
+    const R ex = v[0] - v[2], ey = v[1] - v[3];
     // objective
-    const double w = C.q + (k == 1 ? C.p : 0.0);
-    const double dxg = C.gxg - v[0], dyg = C.gyg - v[1];
-    const double rho2 = dxg * dxg + dyg * dyg, ir2 = 1.0 / rho2;
-    const double gp0 = -dyg * ir2, gp1 = dxg * ir2, phi = a0;
-    double c0 = 0.0, c1 = 0.0, c2 = 0.0, c3 = 0.0;
+    const R w = C.q + (k == 1 ? C.p : R(0));
+    const R dxg = C.gxg - v[0], dyg = C.gyg - v[1];
+    const R rho2 = dxg * dxg + dyg * dyg, ir2 = R(1) / rho2;
+    const R gp0 = -dyg * ir2, gp1 = dxg * ir2, phi = a0;
+    R c0 = R(0), c1 = R(0), c2 = R(0), c3 = R(0);
     if (vel) {
-        c0 = ca; c1 = cb; c2 = da * v[0] + db * v[1]; c3 = type == R_FEN ? C.s : (type == R_FENM ? -C.s : 0.0);
+        c0 = ca; c1 = cb; c2 = da * v[0] + db * v[1]; c3 = type == R_FEN ? C.s : (type == R_FENM ? -C.s : R(0));
     }
     if (obs) {
         c0 = 2 * o[2] * x1 + o[3] * y1; c1 = 2 * o[4] * y1 + o[3] * x1;
@@ -888,13 +1004,13 @@ __device__ __forceinline__ void row_coef(int type, int k, const double (&v)[4], 
     if (type == R_LEG) {
         c0 = 2 * ex; c1 = 2 * ey; c2 = -2 * ex; c3 = -2 * ey;
     }
-    if (type == R_DTH) c3 = 1.0;
+    if (type == R_DTH) c3 = R(1);
     if (type == R_OBJ) {
         c0 = -2 * w * dxg + 2 * C.r * phi * gp0;
         c1 = -2 * w * dyg + 2 * C.r * phi * gp1;
         c2 = 2 * C.r * phi;
-        const double ir4 = ir2 * ir2;
-        const double s00 = 2 * dxg * dyg * ir4, s01 = (dyg * dyg - dxg * dxg) * ir4, s11 = -2 * dxg * dyg * ir4;
+        const R ir4 = ir2 * ir2;
+        const R s00 = 2 * dxg * dyg * ir4, s01 = (dyg * dyg - dxg * dxg) * ir4, s11 = -2 * dxg * dyg * ir4;
         hx[0] = 2 * w + 2 * C.r * (gp0 * gp0 - phi * s00);
         hx[1] = 2 * C.r * (gp0 * gp1 - phi * s01);
         hx[2] = 2 * w + 2 * C.r * (gp1 * gp1 - phi * s11);
@@ -909,32 +1025,32 @@ __device__ __forceinline__ void row_coef(int type, int k, const double (&v)[4], 
 // Hessian blocks of L = f - y^T c: lane kb (0..N) writes S block kb (8x8, symmetric).  Objective parts
 // come from the OBJ rows (hobj), everything else from y and the obstacle forms.
 // ------------------------------------------------------------------------------------------------
-template <int N>
-__device__ void hess_blocks(const WSS<N>& w, int lane, int rps, int nobs, int modi)
+template <int N, class R>
+__device__ void hess_blocks(const WSS<N, R>& w, int lane, int rps, int nobs, int modi)
 {
     if (lane > N) return;
-    const double gm1 = w.cst[K_GM1];
+    const R gm1 = w.cst[K_GM1];
     const int kb = lane;
-    double h00 = 0, h01 = 0, h11 = 0, h04 = 0, h14 = 0, h44 = 0, h24 = 0, h34 = 0;
-    double h05 = 0, h55 = 0;
+    R h00 = 0, h01 = 0, h11 = 0, h04 = 0, h14 = 0, h44 = 0, h24 = 0, h34 = 0;
+    R h05 = 0, h55 = 0;
     if (kb >= 1) {
-        const double* ho = w.hobj + 6 * kb;
+        const R* ho = w.hobj + 6 * kb;
         h00 = ho[0]; h01 = ho[1]; h11 = ho[2]; h04 = ho[3]; h14 = ho[4]; h44 = ho[5];
         // rows of step kb-1 act on x_kb as the post-step state
         const int base = (kb - 1) * rps;
-        const double ct = w.CT[kb], st = w.ST[kb];
-        const double vx = w.V[gx(kb, 2)], vy = w.V[gx(kb, 3)];
-        const double vbx = ct * vx + st * vy, vby = -st * vx + ct * vy;
-        const double wbx = w.ry[base + 0] + (modi ? w.ry[base + rps - 2] + w.ry[base + rps - 1] : 0.0);
-        const double wby = w.ry[base + 1];
+        const R ct = w.CT[kb], st = w.ST[kb];
+        const R vx = w.V[gx(kb, 2)], vy = w.V[gx(kb, 3)];
+        const R vbx = ct * vx + st * vy, vby = -st * vx + ct * vy;
+        const R wbx = w.ry[base + 0] + (modi ? w.ry[base + rps - 2] + w.ry[base + rps - 1] : R(0));
+        const R wby = w.ry[base + 1];
         h24 = wbx * st + wby * ct;
         h34 = -wbx * ct + wby * st;
         h44 += wbx * vbx + wby * vby;
         // inactive slots have y = 0 and a zero form
 #pragma unroll 4
         for (int j = 0; j < nobs; ++j) {
-            const double y = w.ry[base + 2 + j];
-            const double* o = w.obs6 + 6 * j;
+            const R y = w.ry[base + 2 + j];
+            const R* o = w.obs6 + 6 * j;
             h00 -= 2 * y * o[2];
             h01 -= y * o[3];
             h11 -= 2 * y * o[4];
@@ -945,20 +1061,20 @@ __device__ void hess_blocks(const WSS<N>& w, int lane, int rps, int nobs, int mo
         if (kb >= 1) {
 #pragma unroll 4
             for (int j = 0; j < nobs; ++j) {
-                const double y = w.ry[base + 2 + j] * gm1;
-                const double* o = w.obs6 + 6 * j;
+                const R y = w.ry[base + 2 + j] * gm1;
+                const R* o = w.obs6 + 6 * j;
                 h00 -= 2 * y * o[2];
                 h01 -= y * o[3];
                 h11 -= 2 * y * o[4];
             }
         }
-        const double yl = w.ry[base + 2 + nobs];
+        const R yl = w.ry[base + 2 + nobs];
         h00 -= 2 * yl;
         h11 -= 2 * yl;
         h05 = 2 * yl;
         h55 = -2 * yl;
     }
-    double* S = w.S + 64 * kb;
+    R* S = w.S + 64 * kb;
     S[0 * 8 + 0] = h00; S[0 * 8 + 1] = h01; S[1 * 8 + 0] = h01; S[1 * 8 + 1] = h11;
     S[0 * 8 + 4] = h04; S[4 * 8 + 0] = h04; S[1 * 8 + 4] = h14; S[4 * 8 + 1] = h14;
     S[2 * 8 + 4] = h24; S[4 * 8 + 2] = h24; S[3 * 8 + 4] = h34; S[4 * 8 + 3] = h34; S[4 * 8 + 4] = h44;
@@ -974,7 +1090,7 @@ __device__ void hess_blocks(const WSS<N>& w, int lane, int rps, int nobs, int mo
 //   J layout (lane = (g4, col), rows 4s + g4, KSM steps, fully unrolled): J^T y, grad f, J^T w and the
 //   MFMA KKT products.
 // ------------------------------------------------------------------------------------------------
-template <int N, int KSM>
+template <int N, int KSM, class R>
 __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
 {
     using D = Dim<N>;
@@ -988,9 +1104,9 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
     static_assert(NG <= WAVE, "one generator row per lane");
     extern __shared__ __attribute__((aligned(16))) double smem[];
     KP* Ps = reinterpret_cast<KP*>(smem);
-    double* G = smem + KP_DOUBLES;
-    double* E = G + NG * NCP;
-    double* wsb = E + ((NG * 5 + 3) & ~3);
+    R* G = reinterpret_cast<R*>(smem + KP_DOUBLES);
+    R* E = G + NG * NCP;
+    R* wsb = E + ((NG * 5 + 3) & ~3);
     if (threadIdx.x == 0) *Ps = Pv;
     for (int i = threadIdx.x; i < NG * NCP; i += blockDim.x) G[i] = Pv.G[i];
     for (int i = threadIdx.x; i < NG * 5; i += blockDim.x) E[i] = Pv.E[i];
@@ -1005,8 +1121,8 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
     const int mr4 = rfl(P.mr4), mo4 = rfl(P.mo4), m_max = rfl(P.m_max), rps = rfl(P.rps);
     const int nc_max = rfl(P.nc_max), ne_max = rfl(P.ne_max), nobs = nc_max + ne_max;
     const int modi = rfl(P.modi), max_iter = rfl(P.max_iter);
-    WSS<N> w = carve_s<N>(wsb + (size_t)wv * wss_doubles<N>(nc_max, ne_max, mr4, mo4), nc_max, ne_max, mr4, mo4);
-    for (int i = lane; i < 64 * (N + 1); i += WAVE) w.S[i] = 0.0;
+    WSS<N, R> w = carve_s<N, R>(wsb + (size_t)wv * wss_elems<N, R>(nc_max, ne_max, mr4, mo4), nc_max, ne_max, mr4, mo4);
+    for (int i = lane; i < 64 * (N + 1); i += WAVE) w.S[i] = R(0.0);
 
     double gxg, gyg, uj;
     int legv;
@@ -1015,17 +1131,17 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
     // unified quadratic forms per obstacle row slot (zero form for unused slots)
     {
         for (int j = lane; j <= nobs; j += WAVE) {
-            double o[6] = {0, 0, 0, 0, 0, 0};
+            R o[6] = {0, 0, 0, 0, 0, 0};
             if (j < nc_max) {
                 if (j < nc_sel) {
-                    const double* c = w.obs + 3 * j;
-                    o[0] = c[0]; o[1] = c[1]; o[2] = 1.0; o[4] = 1.0; o[5] = c[2] * c[2];
+                    const R* c = w.obs + 3 * j;
+                    o[0] = c[0]; o[1] = c[1]; o[2] = R(1.0); o[4] = R(1.0); o[5] = c[2] * c[2];
                 }
             } else if (j < nobs) {
                 const int e = j - nc_max;
                 if (e < ne_sel) {
-                    const double* el = w.obs + 3 * nc_max + 5 * e;
-                    const double* qq = w.obs + 3 * nc_max + 5 * ne_max;
+                    const R* el = w.obs + 3 * nc_max + 5 * e;
+                    const R* qq = w.obs + 3 * nc_max + 5 * ne_max;
                     o[0] = el[0]; o[1] = el[1];
                     o[2] = qq[e]; o[3] = qq[ne_max + e]; o[4] = qq[2 * ne_max + e]; o[5] = qq[3 * ne_max + e];
                 }
@@ -1062,11 +1178,11 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
     // ---- per-row state (registers)
     int rtype[RPL], rk[RPL], roi[RPL];
     uint32_t rg[RPL];
-    double cl[RPL], cu[RPL], rv[RPL][4], rdv[RPL][4], ra0[RPL], ra1[RPL];
-    double cr[RPL], sr[RPL], zl[RPL], zu[RPL], idl[RPL], idu[RPL];
-    double mu = uni(P.mu_init);
-    double vme = lane < NG ? w.V[lane] : 0.0, dvme = 0.0;   // lane t's generator value / step
-    double th0 = 0.0, nbl = 0.0, mal = 0.0, fo = 0.0, lg0 = 0.0;
+    R cl[RPL], cu[RPL], rv[RPL][4], rdv[RPL][4], ra0[RPL], ra1[RPL];
+    R cr[RPL], sr[RPL], zl[RPL], zu[RPL], idl[RPL], idu[RPL];
+    R mu = uni(R(P.mu_init));
+    R vme = lane < NG ? w.V[lane] : R(0.0), dvme = R(0.0);   // lane t's generator value / step
+    R th0 = R(0.0), nbl = R(0.0), mal = R(0.0), fo = R(0.0), lg0 = R(0.0);
     wave_sync();
 #pragma unroll
     for (int q = 0; q < RPL; ++q) {
@@ -1084,82 +1200,80 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
         roi[q] = ri.type == R_CIR ? ri.slot : (ri.type == R_ELP ? nc_max + ri.slot : 0);
         rg[q] = row_gens(ri.type, ri.k);
         if (r < mo4) w.rgen[r] = rg[q];
-        double clo, cuo;
+        R clo, cuo;
         row_bounds(P, ri, legv, clo, cuo, modi != 0);
         if (r < mr4) {
             w.rclo[r] = clo;
             w.rcuo[r] = cuo;
         }
-        nbl += (double)isfinite(clo) + (double)isfinite(cuo);
-        mal += ri.type < R_NONE ? 1.0 : 0.0;
-        cl[q] = isfinite(clo) ? clo - 1e-8 * fmax(1.0, fabs(clo)) : -INFINITY;
-        cu[q] = isfinite(cuo) ? cuo + 1e-8 * fmax(1.0, fabs(cuo)) : INFINITY;
+        nbl += (R)isfinite(clo) + (R)isfinite(cuo);
+        mal += ri.type < R_NONE ? R(1.0) : R(0.0);
+        cl[q] = isfinite(clo) ? clo - R(1e-8) * fmax(R(1.0), fabs(clo)) : -INFINITY;
+        cu[q] = isfinite(cuo) ? cuo + R(1e-8) * fmax(R(1.0), fabs(cuo)) : INFINITY;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             rv[q][i] = w.V[gen_i(rg[q], i)];
-            rdv[q][i] = 0.0;
+            rdv[q][i] = R(0.0);
         }
-        double o[6];
+        R o[6];
 #pragma unroll
         for (int i = 0; i < 6; ++i) o[i] = w.obs6[6 * roi[q] + i];
         row_trans(rtype[q], rv[q], w.cst[K_GXG], w.cst[K_GYG], ra0[q], ra1[q]);
         cr[q] = row_value(rtype[q], rk[q], rv[q], ra0[q], ra1[q], o, CK);
-        double v = cr[q];
-        const double pl = HL(q) ? fmin(1e-2 * fmax(1.0, fabs(cl[q])), 1e-2 * (cu[q] - cl[q])) : 0.0;
-        const double pu = HU(q) ? fmin(1e-2 * fmax(1.0, fabs(cu[q])), 1e-2 * (cu[q] - cl[q])) : 0.0;
+        R v = cr[q];
+        const R pl = HL(q) ? fmin(R(1e-2) * fmax(R(1.0), fabs(cl[q])), R(1e-2) * (cu[q] - cl[q])) : R(0.0);
+        const R pu = HU(q) ? fmin(R(1e-2) * fmax(R(1.0), fabs(cu[q])), R(1e-2) * (cu[q] - cl[q])) : R(0.0);
         if (HL(q) && HU(q))
             v = fmin(fmax(v, cl[q] + pl), cu[q] - pu);
         else if (HL(q))
             v = fmax(v, cl[q] + pl);
         else if (HU(q))
             v = fmin(v, cu[q] - pu);
-        sr[q] = rtype[q] < R_NONE ? v : 0.0;
-        zl[q] = HL(q) ? 1.0 : 0.0;
-        zu[q] = HU(q) ? 1.0 : 0.0;
-        const double dl = sr[q] - cl[q], du = cu[q] - sr[q];
-        idl[q] = HL(q) ? 1.0 / dl : 0.0;
-        idu[q] = HU(q) ? 1.0 / du : 0.0;
-        lg0 += HL(q) ? (HU(q) ? log(dl * du) : log(dl)) : (HU(q) ? log(du) : 0.0);
+        sr[q] = rtype[q] < R_NONE ? v : R(0.0);
+        zl[q] = HL(q) ? R(1.0) : R(0.0);
+        zu[q] = HU(q) ? R(1.0) : R(0.0);
+        const R dl = sr[q] - cl[q], du = cu[q] - sr[q];
+        idl[q] = HL(q) ? R(1.0) / dl : R(0.0);
+        idu[q] = HU(q) ? R(1.0) / du : R(0.0);
+        lg0 += HL(q) ? (HU(q) ? log(dl * du) : log(dl)) : (HU(q) ? log(du) : R(0.0));
         if (rtype[q] < R_NONE) th0 += fabs(cr[q] - sr[q]);
         if (rtype[q] == R_OBJ) fo += cr[q];
     }
     wsum2(th0, nbl);
     wsum2(fo, lg0);
     mal = wsum(mal);
-    double f_cur = fo, lsum_cur = lg0;
+    R f_cur = fo, lsum_cur = lg0;
     if (lane == 0) {
-        w.cst[K_THMAX] = 1e4 * fmax(1.0, th0);
-        w.cst[K_THMIN] = 1e-4 * fmax(1.0, th0);
+        w.cst[K_THMAX] = R(1e4) * fmax(R(1.0), th0);
+        w.cst[K_THMIN] = R(1e-4) * fmax(R(1.0), th0);
         w.cst[K_MACT] = mal;
         w.cst[K_NBL] = nbl;
     }
     wave_sync();
-    double fth0 = INFINITY, fph0 = INFINITY, fth1 = INFINITY, fph1 = INFINITY;   // filter entries lane, lane+64
+    R fth0 = INFINITY, fph0 = INFINITY, fth1 = INFINITY, fph1 = INFINITY;   // filter entries lane, lane+64
     int nf = 0;
-    double dw_last = 0.0;
+    R dw_last = R(0.0);
     int status = -1, it = 0, n_rest = 0;
-    double e0 = INFINITY;
-    const double gth = 1e-5, gph = 1e-8, sth = 1.1, sph = 2.3, eta = 1e-8, gal = 0.05;
+    R e0 = INFINITY;
+    const R gth = R(1e-5), gph = R(1e-8), sth = R(1.1), sph = R(2.3), eta = R(1e-8), gal = R(0.05);
 
     STAMP_DECL
     for (it = 0; it <= max_iter; ++it) {
-        double gl[NT];                                  // J^T y - grad f  (per column, all lanes)
-        double jv[JC ? KSM : 1][NT];
+        R gl[NT];                                  // J^T y - grad f  (per column, all lanes)
+        R jv[JC ? KSM : 1][NT];
         for (;;) {
             RELANE();
             // ---- row layout: generator-form coefficients at V (OBJ rows: grad f_k and its Hessian parts)
 #pragma unroll
             for (int q = 0; q < RPL; ++q) {
                 const int r = lane + WAVE * q;
-                double o[6], cf[4], hx[6];
+                R o[6], cf[4], hx[6];
 #pragma unroll
                 for (int i = 0; i < 6; ++i) o[i] = w.obs6[6 * roi[q] + i];
                 row_coef(rtype[q], rk[q], rv[q], ra0[q], ra1[q], o, CK, cf, hx);
                 if (r < mo4) {
-                    double2* rc2 = reinterpret_cast<double2*>(w.rcoef + 4 * r);
-                    rc2[0] = make_double2(cf[0], cf[1]);
-                    rc2[1] = make_double2(cf[2], cf[3]);
-                    w.ry[r] = rtype[q] == R_OBJ ? -1.0 : zl[q] - zu[q];
+                    st4(w.rcoef + 4 * r, cf[0], cf[1], cf[2], cf[3]);
+                    w.ry[r] = rtype[q] == R_OBJ ? -R(1.0) : zl[q] - zu[q];
                 }
                 if (rtype[q] == R_VBX) {
                     w.CT[rk[q] + 1] = ra1[q];
@@ -1175,20 +1289,20 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
             RELANE();
             // ---- J layout: gl = J^T y - grad f (OBJ rows carry y = -1)
 #pragma unroll
-            for (int T = 0; T < NT; ++T) gl[T] = 0.0;
+            for (int T = 0; T < NT; ++T) gl[T] = R(0.0);
             // mo4 == 4 * KSM: every step is a real (possibly padding) row group -> one basic block,
             // all loads in flight together
 #pragma unroll
             for (int s = 0; s < KSM; ++s) {
                 const int r = 4 * s + g4;
                 const uint32_t pk = w.rgen[r];
-                const double2* rc2 = reinterpret_cast<const double2*>(w.rcoef + 4 * r);
-                const double2 ca = rc2[0], cb = rc2[1];
-                const double y = w.ry[r];
+                struct { R x, y; } ca, cb;
+                ld4(w.rcoef + 4 * r, ca.x, ca.y, cb.x, cb.y);
+                const R y = w.ry[r];
 #pragma unroll
                 for (int T = 0; T < NT; ++T) {
                     const int cc = 16 * T + col;
-                    const double j = ca.x * G[gen_i(pk, 0) * NCP + cc] + ca.y * G[gen_i(pk, 1) * NCP + cc] +
+                    const R j = ca.x * G[gen_i(pk, 0) * NCP + cc] + ca.y * G[gen_i(pk, 1) * NCP + cc] +
                                      cb.x * G[gen_i(pk, 2) * NCP + cc] + cb.y * G[gen_i(pk, 3) * NCP + cc];
                     gl[T] += j * y;
                     if constexpr (JC) jv[JC ? s : 0][T] = j;
@@ -1199,14 +1313,14 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
             STAMP(1);
             // ---- convergence test (IPOPT scaled overall error) and barrier update
             RELANE();
-            double ru = 0.0;
+            R ru = R(0.0);
 #pragma unroll
             for (int T = 0; T < NT; ++T)
                 if (g4 == 0 && 16 * T + col < n) ru = fmax(ru, fabs(gl[T]));
-            double rcm = 0.0, nz = 0.0, comp0 = 0.0;
+            R rcm = R(0.0), nz = R(0.0), comp0 = R(0.0);
 #pragma unroll
             for (int q = 0; q < RPL; ++q) {
-                const double dl = sr[q] - cl[q], du = cu[q] - sr[q];
+                const R dl = sr[q] - cl[q], du = cu[q] - sr[q];
                 if (rtype[q] < R_NONE) rcm = fmax(rcm, fabs(cr[q] - sr[q]));
                 nz += fabs(zl[q]) + fabs(zu[q]);
                 if (HL(q)) comp0 = fmax(comp0, fabs(dl * zl[q]));
@@ -1216,28 +1330,28 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
             rcm = wmax(rcm);
             nz = wsum(nz);
             comp0 = wmax(comp0);
-            const double sd = uni(fmax(100.0, nz / (w.cst[K_MACT] + n)) / 100.0);
-            const double sc = uni(fmax(100.0, nz / fmax(1.0, w.cst[K_NBL])) / 100.0);
-            const double base_err = uni(fmax(ru / sd, rcm));
+            const R sd = uni(fmax(R(100.0), nz / (w.cst[K_MACT] + n)) / R(100.0));
+            const R sc = uni(fmax(R(100.0), nz / fmax(R(1.0), w.cst[K_NBL])) / R(100.0));
+            const R base_err = uni(fmax(ru / sd, rcm));
             e0 = uni(fmax(base_err, comp0 / sc));
             if (e0 <= w.cst[K_TOL]) {
                 status = 0;
                 break;
             }
             if (it == max_iter) break;
-            const double mu_min = w.cst[K_TOL] / 10.0;
-            const double mu_prev = mu;
+            const R mu_min = w.cst[K_TOL] / R(10.0);
+            const R mu_prev = mu;
             for (int t = 0; t < 8; ++t) {
-                double cm = 0.0;
+                R cm = R(0.0);
 #pragma unroll
                 for (int q = 0; q < RPL; ++q) {
-                    const double dl = sr[q] - cl[q], du = cu[q] - sr[q];
+                    const R dl = sr[q] - cl[q], du = cu[q] - sr[q];
                     if (HL(q)) cm = fmax(cm, fabs(dl * zl[q] - mu));
                     if (HU(q)) cm = fmax(cm, fabs(du * zu[q] - mu));
                 }
                 cm = wmax(cm);
-                if (fmax(base_err, cm / sc) <= 10.0 * mu && mu > mu_min)
-                    mu = uni(fmax(mu_min, fmin(0.2 * mu, mu * sqrt(mu))));
+                if (fmax(base_err, cm / sc) <= R(10.0) * mu && mu > mu_min)
+                    mu = uni(fmax(mu_min, fmin(R(0.2) * mu, mu * sqrt(mu))));
                 else
                     break;
             }
@@ -1246,52 +1360,52 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
         }
         STAMP(2);
         if (status == 0 || it == max_iter) break;
-        const double tau = uni(fmax(0.99, 1.0 - mu));
+        const R tau = uni(fmax(R(0.99), R(1.0) - mu));
 
         // ---- Sigma, rhs weights, Hessian blocks
         RELANE();
-        double rcv[RPL];
+        R rcv[RPL];
 #pragma unroll
         for (int q = 0; q < RPL; ++q) {
             const int r = lane + WAVE * q;
-            const double sg = zl[q] * idl[q] + zu[q] * idu[q];
-            rcv[q] = rtype[q] < R_NONE ? cr[q] - sr[q] : 0.0;
-            double wr = mu * idl[q] - mu * idu[q] - sg * rcv[q];
-            wr = rtype[q] == R_OBJ ? -1.0 : wr;
+            const R sg = zl[q] * idl[q] + zu[q] * idu[q];
+            rcv[q] = rtype[q] < R_NONE ? cr[q] - sr[q] : R(0.0);
+            R wr = mu * idl[q] - mu * idu[q] - sg * rcv[q];
+            wr = rtype[q] == R_OBJ ? -R(1.0) : wr;
             if (r < mo4) {
                 w.rsig[r] = sg;
                 w.rw[r] = wr;
             }
         }
         RELANE();
-        hess_blocks<N>(w, lane, rps, nobs, modi);
+        hess_blocks<N, R>(w, lane, rps, nobs, modi);
         wave_sync();
         STAMP(3);
         // ---- K = J^T Sigma J + G^T S G by f64 MFMA (two accumulator chains), rhs = J^T w - grad f
-        double rhsc[NT];
+        R rhsc[NT];
         RELANE();
         {
             constexpr int NA = NT * (NT + 1) / 2;
-            d4 acc[2][NA];
+            typename Mfma<R>::acc acc[2][NA];
 #pragma unroll
             for (int h = 0; h < 2; ++h)
 #pragma unroll
-                for (int i = 0; i < NA; ++i) acc[h][i] = d4{0.0, 0.0, 0.0, 0.0};
-            double pw[NT];
+                for (int i = 0; i < NA; ++i) acc[h][i] = typename Mfma<R>::acc{R(0), R(0), R(0), R(0)};
+            R pw[NT];
 #pragma unroll
-            for (int T = 0; T < NT; ++T) pw[T] = 0.0;
+            for (int T = 0; T < NT; ++T) pw[T] = R(0.0);
 #pragma unroll
             for (int s = 0; s < KSM; ++s) {
                 const int r = 4 * s + g4;
-                const double sg = w.rsig[r], wr = w.rw[r];   // padding / OBJ rows: sigma = 0
-                double j[NT];
+                const R sg = w.rsig[r], wr = w.rw[r];   // padding / OBJ rows: sigma = 0
+                R j[NT];
                 if constexpr (JC) {
 #pragma unroll
                     for (int T = 0; T < NT; ++T) j[T] = jv[JC ? s : 0][T];
                 } else {
                     const uint32_t pk = w.rgen[r];
-                    const double2* rc2 = reinterpret_cast<const double2*>(w.rcoef + 4 * r);
-                    const double2 ca = rc2[0], cb = rc2[1];
+                    struct { R x, y; } ca, cb;
+                    ld4(w.rcoef + 4 * r, ca.x, ca.y, cb.x, cb.y);
 #pragma unroll
                     for (int T = 0; T < NT; ++T) {
                         const int cc = 16 * T + col;
@@ -1301,44 +1415,44 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
                 }
 #pragma unroll
                 for (int T = 0; T < NT; ++T) pw[T] += j[T] * wr;
-                d4* a = acc[s & 1];
-                a[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(j[0], sg * j[0], a[0], 0, 0, 0);
+                auto* a = acc[s & 1];
+                a[0] = Mfma<R>::run(j[0], sg * j[0], a[0]);
                 if constexpr (NT == 2) {
-                    a[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(j[0], sg * j[1], a[1], 0, 0, 0);
-                    a[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(j[1], sg * j[1], a[2], 0, 0, 0);
+                    a[1] = Mfma<R>::run(j[0], sg * j[1], a[1]);
+                    a[2] = Mfma<R>::run(j[1], sg * j[1], a[2]);
                 }
             }
 #pragma unroll
             for (int s = 1; s < NG / 4; ++s) {
                 const int t = 4 * s + g4;
                 const int kb = t >> 3, c = t & 7;
-                const double* Srow = w.S + 64 * kb + 8 * c;
-                const double* Gb = G + 8 * kb * NCP;
-                double gv[NT], sgv[NT];
+                const R* Srow = w.S + 64 * kb + 8 * c;
+                const R* Gb = G + 8 * kb * NCP;
+                R gv[NT], sgv[NT];
 #pragma unroll
                 for (int T = 0; T < NT; ++T) {
                     gv[T] = G[t * NCP + 16 * T + col];
-                    double a = 0.0;
+                    R a = R(0.0);
 #pragma unroll
                     for (int c2 = 0; c2 < 8; ++c2) a += Srow[c2] * Gb[c2 * NCP + 16 * T + col];
                     sgv[T] = a;
                 }
-                d4* a = acc[s & 1];
-                a[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(gv[0], sgv[0], a[0], 0, 0, 0);
+                auto* a = acc[s & 1];
+                a[0] = Mfma<R>::run(gv[0], sgv[0], a[0]);
                 if constexpr (NT == 2) {
-                    a[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(gv[0], sgv[1], a[1], 0, 0, 0);
-                    a[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(gv[1], sgv[1], a[2], 0, 0, 0);
+                    a[1] = Mfma<R>::run(gv[0], sgv[1], a[1]);
+                    a[2] = Mfma<R>::run(gv[1], sgv[1], a[2]);
                 }
             }
 #pragma unroll
             for (int T = 0; T < NT; ++T) rhsc[T] = gsum(pw[T]);
-            // C/D layout of v_mfma_f64_16x16x4: lane holds D[g4 + 4*i][col], i = 0..3
+            // C/D layout (Mfma<R>::row): f64 lane holds D[g4 + 4*i][col], f32 D[4*g4 + i][col], i = 0..3
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const int row = g4 + 4 * i;
+                const int row = Mfma<R>::row(g4, i);
                 w.K[row * KLD + col] = acc[0][0][i] + acc[1][0][i];
                 if constexpr (NT == 2) {
-                    const double k1 = acc[0][1][i] + acc[1][1][i];
+                    const R k1 = acc[0][1][i] + acc[1][1][i];
                     w.K[row * KLD + 16 + col] = k1;
                     w.K[(16 + col) * KLD + row] = k1;
                     w.K[(16 + row) * KLD + 16 + col] = acc[0][2][i] + acc[1][2][i];
@@ -1349,100 +1463,100 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
         STAMP(4);
         // ---- factor with inertia correction, solve for dp
         RELANE();
-        double xv;
+        R xv;
         {
-            double rhs_l = 0.0;
+            R rhs_l = R(0.0);
 #pragma unroll
             for (int T = 0; T < NT; ++T) rhs_l = (lane < n && (lane >> 4) == T) ? rhsc[T] : rhs_l;
-            double a[n];
-            double myidg = 1.0;
+            R a[n];
+            R myidg = R(1.0);
 #pragma unroll
-            for (int j = 0; j < n; ++j) a[j] = lane < n ? w.K[lane * KLD + j] : (lane == j ? 1.0 : 0.0);
+            for (int j = 0; j < n; ++j) a[j] = lane < n ? w.K[lane * KLD + j] : (lane == j ? R(1.0) : R(0.0));
             if (!chol_rows<n>(a, myidg, lane)) {
-                double dw = dw_last == 0.0 ? 1e-4 : fmax(1e-20, dw_last / 3.0);
+                R dw = dw_last == R(0.0) ? R(1e-4) : fmax(R(1e-20), dw_last / R(3.0));
                 for (;;) {
 #pragma unroll
                     for (int j = 0; j < n; ++j)
-                        a[j] = (lane < n ? w.K[lane * KLD + j] : (lane == j ? 1.0 : 0.0)) + (lane == j ? dw : 0.0);
+                        a[j] = (lane < n ? w.K[lane * KLD + j] : (lane == j ? R(1.0) : R(0.0))) + (lane == j ? dw : R(0.0));
                     if (chol_rows<n>(a, myidg, lane)) break;
-                    dw *= dw_last == 0.0 ? 100.0 : 8.0;
-                    if (dw > 1e40) break;
+                    dw *= dw_last == R(0.0) ? R(100.0) : R(8.0);
+                    if (dw > R(sizeof(R) == 8 ? 1e40 : 1e30)) break;
                 }
                 dw_last = uni(dw);
             }
             // forward: L y = rhs
-            double acc = 0.0, yv = 0.0;
+            R acc = R(0.0), yv = R(0.0);
 #pragma unroll
             for (int k = 0; k < n; ++k) {
-                const double yk = bcast((rhs_l - acc) * myidg, k);
+                const R yk = bcast((rhs_l - acc) * myidg, k);
                 yv = lane == k ? yk : yv;
-                acc += lane > k ? a[k] * yk : 0.0;
+                acc += lane > k ? a[k] * yk : R(0.0);
             }
             // transpose L through LDS for the backward sweep
             wave_sync();
             if (lane < n) {
 #pragma unroll
-                for (int j = 0; j < n; ++j) w.K[lane * KLD + j] = j <= lane ? a[j] : 0.0;
+                for (int j = 0; j < n; ++j) w.K[lane * KLD + j] = j <= lane ? a[j] : R(0.0);
             }
             wave_sync();
-            acc = 0.0;
-            xv = 0.0;
+            acc = R(0.0);
+            xv = R(0.0);
 #pragma unroll
             for (int i = n - 1; i >= 0; --i) {
-                const double xi = bcast((yv - acc) * myidg, i);
+                const R xi = bcast((yv - acc) * myidg, i);
                 xv = lane == i ? xi : xv;
-                acc += lane < i ? w.K[i * KLD + (lane & 31)] * xi : 0.0;
+                acc += lane < i ? w.K[i * KLD + (lane & 31)] * xi : R(0.0);
             }
         }
         STAMP(5);
         // ---- dV = G dp (lane t), rows pick up their 4 entries
         RELANE();
         {
-            double v = 0.0;
+            R v = R(0.0);
 #pragma unroll
             for (int j = 0; j < n; ++j) v += G[(lane < NG ? lane : 0) * NCP + j] * bcast(xv, j);
-            dvme = lane < NG ? v : 0.0;
+            dvme = lane < NG ? v : R(0.0);
             if (lane < NG) w.dV[lane] = dvme;
         }
         wave_sync();
         // ---- slack / multiplier steps, fraction to boundary
         RELANE();
-        double dS[RPL], dZl[RPL], dZu[RPL];
-        double ap = 1.0, az = 1.0, theta = 0.0, sl = 0.0, gdv = 0.0;
+        R dS[RPL], dZl[RPL], dZu[RPL];
+        R ap = R(1.0), az = R(1.0), theta = R(0.0), sl = R(0.0), gdv = R(0.0);
 #pragma unroll
         for (int q = 0; q < RPL; ++q) {
             const int r = lane + WAVE * q;
 #pragma unroll
             for (int i = 0; i < 4; ++i) rdv[q][i] = w.dV[gen_i(rg[q], i)];
-            double jd = 0.0;
+            R jd = R(0.0);
             if (r < mo4) {
-                const double2* rc2 = reinterpret_cast<const double2*>(w.rcoef + 4 * r);
-                const double2 ca = rc2[0], cb = rc2[1];
+                struct { R x, y; } ca, cb;
+                ld4(w.rcoef + 4 * r, ca.x, ca.y, cb.x, cb.y);
                 jd = ca.x * rdv[q][0] + ca.y * rdv[q][1] + cb.x * rdv[q][2] + cb.y * rdv[q][3];
             }
             if (rtype[q] == R_OBJ) gdv += jd;
-            dS[q] = rtype[q] < R_NONE ? jd + rcv[q] : 0.0;
-            dZl[q] = HL(q) ? mu * idl[q] - zl[q] - zl[q] * idl[q] * dS[q] : 0.0;
-            dZu[q] = HU(q) ? mu * idu[q] - zu[q] + zu[q] * idu[q] * dS[q] : 0.0;
-            const double dl = sr[q] - cl[q], du = cu[q] - sr[q];
-            const double ids = rcp_nr(dS[q]);
+            dS[q] = rtype[q] < R_NONE ? jd + rcv[q] : R(0.0);
+            dZl[q] = HL(q) ? mu * idl[q] - zl[q] - zl[q] * idl[q] * dS[q] : R(0.0);
+            dZu[q] = HU(q) ? mu * idu[q] - zu[q] + zu[q] * idu[q] * dS[q] : R(0.0);
+            const R dl = sr[q] - cl[q], du = cu[q] - sr[q];
+            const R ids = rcp_nr(dS[q]);
             if (HL(q) && dS[q] < 0) ap = fmin(ap, -tau * dl * ids);
             if (HU(q) && dS[q] > 0) ap = fmin(ap, tau * du * ids);
             if (HL(q) && dZl[q] < 0) az = fmin(az, -tau * zl[q] * rcp_nr(dZl[q]));
             if (HU(q) && dZu[q] < 0) az = fmin(az, -tau * zu[q] * rcp_nr(dZu[q]));
             theta += fabs(rcv[q]);
-            sl += (HL(q) ? dS[q] * idl[q] : 0.0) - (HU(q) ? dS[q] * idu[q] : 0.0);
+            sl += (HL(q) ? dS[q] * idl[q] : R(0.0)) - (HU(q) ? dS[q] * idu[q] : R(0.0));
         }
         ap = wmin(ap);
         az = wmin(az);
         wsum2(theta, gdv);
         sl = wsum(sl);
-        const double phi = uni(f_cur - mu * lsum_cur);
-        const double gphi = uni(gdv - mu * sl);
+        const R phi = uni(f_cur - mu * lsum_cur);
+        const R gphi = uni(gdv - mu * sl);
         // switching condition a (-gphi)^s_phi > theta^s_theta in log space: log a + s_phi log(-gphi) >
         // s_theta log theta (two logs per iteration instead of two pow per trial)
-        const double lsw = uni(gphi < 0 ? sth * log(theta) - sph * log(-gphi) : 0.0);
-        double amin;
+        const R lsw = uni(gphi < 0 ? sth * log(theta) - sph * log(-gphi) : R(0.0));
+        R amin;
         if (gphi < 0) {
             amin = fmin(gth, gph * theta / -gphi);
             if (theta <= w.cst[K_THMIN]) amin = fmin(amin, exp(lsw));
@@ -1452,38 +1566,38 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
         amin = uni(amin * gal);
         STAMP(6);
         // ---- filter line search on trial points V + a dV (row registers only)
-        double a = ap;
-        double la = uni(log(ap));   // log a, tracked exactly through the halvings
+        R a = ap;
+        R la = uni(log(ap));   // log a, tracked exactly through the halvings
         bool accepted = false, ftype = false;
-        double ctr[RPL], ta0[RPL], ta1[RPL], vt[RPL][4];
-        double ft = 0.0, lgt = 0.0;
+        R ctr[RPL], ta0[RPL], ta1[RPL], vt[RPL][4];
+        R ft = R(0.0), lgt = R(0.0);
         while (a >= amin) {
             RELANE();
-            double tht = 0.0;
-            ft = 0.0;
-            lgt = 0.0;
+            R tht = R(0.0);
+            ft = R(0.0);
+            lgt = R(0.0);
             bool bad = false;
 #pragma unroll
             for (int q = 0; q < RPL; ++q) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) vt[q][i] = fma(a, rdv[q][i], rv[q][i]);
-                double o[6];
+                R o[6];
 #pragma unroll
                 for (int i = 0; i < 6; ++i) o[i] = w.obs6[6 * roi[q] + i];
                 row_trans(rtype[q], vt[q], w.cst[K_GXG], w.cst[K_GYG], ta0[q], ta1[q]);
                 ctr[q] = row_value(rtype[q], rk[q], vt[q], ta0[q], ta1[q], o, CK);
-                const double st = sr[q] + a * dS[q];
+                const R st = sr[q] + a * dS[q];
                 if (rtype[q] < R_NONE) tht += fabs(ctr[q] - st);
                 if (rtype[q] == R_OBJ) ft += ctr[q];
-                const double d1 = st - cl[q], d2 = cu[q] - st;
+                const R d1 = st - cl[q], d2 = cu[q] - st;
                 if (HL(q) && !(d1 > 0)) bad = true;
                 if (HU(q) && !(d2 > 0)) bad = true;
-                lgt += HL(q) ? (HU(q) ? log(d1 * d2) : log(d1)) : (HU(q) ? log(d2) : 0.0);
+                lgt += HL(q) ? (HU(q) ? log(d1 * d2) : log(d1)) : (HU(q) ? log(d2) : R(0.0));
             }
             wsum2(ft, tht);
             lgt = wsum(lgt);
             const bool anybad = __ballot(bad) != 0ull;
-            const double pht = anybad ? INFINITY : ft - mu * lgt;
+            const R pht = anybad ? INFINITY : ft - mu * lgt;
             bool ok = isfinite(pht) && tht < w.cst[K_THMAX];
             if (ok) {
                 const bool b0 = lane < nf && !(tht < fth0 || pht < fph0);
@@ -1503,14 +1617,14 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
                 }
             }
             if (accepted) break;
-            a = uni(a * 0.5);
-            la = uni(la - M_LN2);
+            a = uni(a * R(0.5));
+            la = uni(la - R(M_LN2));
         }
         STAMP(7);
         RELANE();
         if (accepted) {
             if (!ftype && nf < FILTER_CAP) {
-                const double fvt = (1 - gth) * theta, fvp = phi - gph * theta;
+                const R fvt = (1 - gth) * theta, fvp = phi - gph * theta;
                 if ((nf & (WAVE - 1)) == lane) {
                     if (nf < WAVE) {
                         fth0 = fvt;
@@ -1538,28 +1652,28 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
             // restoration substitute: shortest tried step, slacks reset onto c(u), filter reset
             a = uni(fmax(a, amin));
             vme = fma(a, dvme, vme);
-            double fr = 0.0, lr = 0.0;
+            R fr = R(0.0), lr = R(0.0);
 #pragma unroll
             for (int q = 0; q < RPL; ++q) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) rv[q][i] = fma(a, rdv[q][i], rv[q][i]);
-                double o[6];
+                R o[6];
 #pragma unroll
                 for (int i = 0; i < 6; ++i) o[i] = w.obs6[6 * roi[q] + i];
                 row_trans(rtype[q], rv[q], w.cst[K_GXG], w.cst[K_GYG], ra0[q], ra1[q]);
                 cr[q] = row_value(rtype[q], rk[q], rv[q], ra0[q], ra1[q], o, CK);
-                double v = cr[q];
-                const double pl = HL(q) ? fmin(1e-2 * fmax(1.0, fabs(cl[q])), 1e-2 * (cu[q] - cl[q])) : 0.0;
-                const double pu = HU(q) ? fmin(1e-2 * fmax(1.0, fabs(cu[q])), 1e-2 * (cu[q] - cl[q])) : 0.0;
+                R v = cr[q];
+                const R pl = HL(q) ? fmin(R(1e-2) * fmax(R(1.0), fabs(cl[q])), R(1e-2) * (cu[q] - cl[q])) : R(0.0);
+                const R pu = HU(q) ? fmin(R(1e-2) * fmax(R(1.0), fabs(cu[q])), R(1e-2) * (cu[q] - cl[q])) : R(0.0);
                 if (HL(q) && HU(q))
                     v = fmin(fmax(v, cl[q] + pl), cu[q] - pu);
                 else if (HL(q))
                     v = fmax(v, cl[q] + pl);
                 else if (HU(q))
                     v = fmin(v, cu[q] - pu);
-                sr[q] = rtype[q] < R_NONE ? v : 0.0;
-                const double d1 = sr[q] - cl[q], d2 = cu[q] - sr[q];
-                lr += HL(q) ? (HU(q) ? log(d1 * d2) : log(d1)) : (HU(q) ? log(d2) : 0.0);
+                sr[q] = rtype[q] < R_NONE ? v : R(0.0);
+                const R d1 = sr[q] - cl[q], d2 = cu[q] - sr[q];
+                lr += HL(q) ? (HU(q) ? log(d1 * d2) : log(d1)) : (HU(q) ? log(d2) : R(0.0));
                 if (rtype[q] == R_OBJ) fr += cr[q];
             }
             wsum2(fr, lr);
@@ -1568,7 +1682,7 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
             nf = 0;
             // infeasibility detection (stands in for IPOPT's failed restoration phase)
             n_rest++;
-            double viol = 0.0;
+            R viol = R(0.0);
 #pragma unroll
             for (int q = 0; q < RPL; ++q) {
                 const int r = lane + WAVE * q;
@@ -1578,7 +1692,7 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
                 }
             }
             viol = wmax(viol);
-            if (n_rest >= REST_FAIL && viol > 1e-4) {
+            if (n_rest >= REST_FAIL && viol > R(1e-4)) {
                 if (lane < NG) w.V[lane] = vme;
                 status = 2;
                 it++;
@@ -1590,11 +1704,11 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
         for (int q = 0; q < RPL; ++q) {
             zl[q] += az * dZl[q];
             zu[q] += az * dZu[q];
-            const double d1 = sr[q] - cl[q], d2 = cu[q] - sr[q];
-            idl[q] = HL(q) ? rcp_nr(d1) : 0.0;
-            idu[q] = HU(q) ? rcp_nr(d2) : 0.0;
-            zl[q] = HL(q) ? fmin(fmax(zl[q], mu * 1e-10 * idl[q]), 1e10 * mu * idl[q]) : 0.0;
-            zu[q] = HU(q) ? fmin(fmax(zu[q], mu * 1e-10 * idu[q]), 1e10 * mu * idu[q]) : 0.0;
+            const R d1 = sr[q] - cl[q], d2 = cu[q] - sr[q];
+            idl[q] = HL(q) ? rcp_nr(d1) : R(0.0);
+            idu[q] = HU(q) ? rcp_nr(d2) : R(0.0);
+            zl[q] = HL(q) ? fmin(fmax(zl[q], mu * R(1e-10) * idl[q]), R(1e10) * mu * idl[q]) : R(0.0);
+            zu[q] = HU(q) ? fmin(fmax(zu[q], mu * R(1e-10) * idu[q]), R(1e10) * mu * idu[q]) : R(0.0);
         }
         wave_sync();
         STAMP(9);
@@ -1605,14 +1719,14 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
     wave_sync();
     RELANE();
     if (status != 0 && status != 2) {
-        double viol = 0.0;
+        R viol = R(0.0);
 #pragma unroll
         for (int q = 0; q < RPL; ++q) {
             const int r = lane + WAVE * q;
-            double o[6];
+            R o[6];
 #pragma unroll
             for (int i = 0; i < 6; ++i) o[i] = w.obs6[6 * roi[q] + i];
-            const double c = row_value(rtype[q], rk[q], rv[q], ra0[q], ra1[q], o, CK);
+            const R c = row_value(rtype[q], rk[q], rv[q], ra0[q], ra1[q], o, CK);
             if (r < mr4 && rtype[q] < R_NONE) {
                 if (HL(q)) viol = fmax(viol, w.rclo[r] - c);
                 if (HU(q)) viol = fmax(viol, c - w.rcuo[r]);
@@ -1621,7 +1735,7 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
         viol = wmax(viol);
         if (e0 <= w.cst[K_ACCTOL])
             status = 1;
-        else if (viol > 1e-4)
+        else if (viol > R(1e-4))
             status = 2;
     }
     // canonical u: u_k = x_{k+1} (W u_k = p_k since W B = I) — the reference's "desired next state"
@@ -2649,6 +2763,7 @@ __global__ __launch_bounds__(256, 4) void dd_eval_kernel(KP Pv)
     }
 }
 
+#if ALIP_PART_HOST
 // ------------------------------------------------------------------------------------------------
 // closed-loop rollout ("data_log replay" batch harness): after each solve, every
 // active instance executes its first planned step on an ideal ALIP plant and re-plans from the touchdown
@@ -2748,9 +2863,126 @@ __global__ __launch_bounds__(256) void rollout_init_kernel(long long B, int S, i
     if (xtraj)
         for (int i = 0; i < sd; ++i) xtraj[(size_t)b * (S + 1) * sd + i] = x0[(size_t)b * sd + i];
 }
+#endif  // ALIP_PART_HOST
+
+// ------------------------------------------------------------------------------------------------
+// kernel launchers.  The library may be built as one translation unit per horizon N (ALIP_PART = N:
+// that horizon's kernels and launch_lip_N / launch_dd_N) plus ALIP_PART = 0 (host code, C ABI, rollout
+// kernels), compiled in parallel and linked into one .so; without ALIP_PART everything is one TU.
+// ------------------------------------------------------------------------------------------------
+// dynamic-LDS opt-in, once per kernel and size (hipFuncSetAttribute is a host round trip: keep it out of the
+// steady-state launch path)
+static void set_smem(const void* f, size_t smem)
+{
+    static std::mutex mtx;
+    static std::unordered_map<const void*, size_t> done[64];   // per device ordinal
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(mtx);
+    auto& d = done[dev & 63];
+    auto it = d.find(f);
+    if (it != d.end() && it->second >= smem) return;
+    (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    d[f] = smem;
+}
+
+template <int N, class R>
+void launch_solve(const KP& P, size_t smem, hipStream_t st)
+{
+    const unsigned grid = (unsigned)((P.B + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
+    {
+        // KSM = 4-row steps of the J layout, the smallest compiled size covering mo4 rows
+        auto go = [&](auto kern) {
+            set_smem((const void*)kern, smem);
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(WAVE * WAVES_PER_BLOCK), smem, st, P);
+        };
+        if (P.mo4 <= 32)
+            go(solve_kernel<N, 8, R>);
+        else if (P.mo4 <= 40)
+            go(solve_kernel<N, 10, R>);
+        else if (P.mo4 <= 48)
+            go(solve_kernel<N, 12, R>);
+        else if (P.mo4 <= 64)
+            go(solve_kernel<N, 16, R>);
+        else if (P.mo4 <= 96)
+            go(solve_kernel<N, 24, R>);
+        else if (P.mo4 <= 128)
+            go(solve_kernel<N, 32, R>);
+        else
+            go(solve_kernel<N, 48, R>);
+    }
+}
+
+// solve kernels run in the handle's precision (cfg.precision); the eval hook is always fp64
+template <int N>
+hipError_t launch_t(bool solve, bool f32, const KP& P, size_t smem, hipStream_t st)
+{
+    const unsigned grid = (unsigned)((P.B + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
+    if (solve && f32) {
+        launch_solve<N, float>(P, smem, st);
+    } else if (solve) {
+        launch_solve<N, double>(P, smem, st);
+    } else {
+        set_smem((const void*)eval_kernel<N>, smem);
+        hipLaunchKernelGGL(eval_kernel<N>, dim3(grid), dim3(WAVE * WAVES_PER_BLOCK), smem, st, P);
+    }
+    return hipGetLastError();
+}
+
+template <int N>
+hipError_t launch_dd(bool solve, const KP& P, size_t smem, hipStream_t st)
+{
+    const unsigned grid = (unsigned)((P.B + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
+    auto go = [&](auto kern) {
+        set_smem((const void*)kern, smem);
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(WAVE * WAVES_PER_BLOCK), smem, st, P);
+    };
+    if (!solve)
+        go(dd_eval_kernel<N>);
+    else if (P.mo4 <= WAVE)
+        go(dd_solve_kernel<N, 1>);
+    else if (P.mo4 <= 2 * WAVE)
+        go(dd_solve_kernel<N, 2>);
+    else
+        go(dd_solve_kernel<N, 3>);
+    return hipGetLastError();
+}
+
+#define ALIP_LAUNCHERS(k)                                                                              \
+    hipError_t launch_lip_##k(bool solve, bool f32, const KP& P, size_t smem, hipStream_t st)          \
+    {                                                                                                  \
+        return launch_t<k>(solve, f32, P, smem, st);                                                   \
+    }                                                                                                  \
+    hipError_t launch_dd_##k(bool solve, const KP& P, size_t smem, hipStream_t st)                     \
+    {                                                                                                  \
+        return launch_dd<k>(solve, P, smem, st);                                                       \
+    }
+#define ALIP_LAUNCH_DECL(k)                                                                            \
+    hipError_t launch_lip_##k(bool solve, bool f32, const KP& P, size_t smem, hipStream_t st);         \
+    hipError_t launch_dd_##k(bool solve, const KP& P, size_t smem, hipStream_t st);
+ALIP_LAUNCH_DECL(1) ALIP_LAUNCH_DECL(2) ALIP_LAUNCH_DECL(3) ALIP_LAUNCH_DECL(4) ALIP_LAUNCH_DECL(5) ALIP_LAUNCH_DECL(6)
+#if ALIP_PART_N(1)
+ALIP_LAUNCHERS(1)
+#endif
+#if ALIP_PART_N(2)
+ALIP_LAUNCHERS(2)
+#endif
+#if ALIP_PART_N(3)
+ALIP_LAUNCHERS(3)
+#endif
+#if ALIP_PART_N(4)
+ALIP_LAUNCHERS(4)
+#endif
+#if ALIP_PART_N(5)
+ALIP_LAUNCHERS(5)
+#endif
+#if ALIP_PART_N(6)
+ALIP_LAUNCHERS(6)
+#endif
 
 }  // namespace alip
 
+#if ALIP_PART_HOST
 // ================================================================================================
 // host side: constants, handle, C ABI
 // ================================================================================================
@@ -2888,11 +3120,13 @@ size_t smem_bytes(const Handle* h, bool solve)
         (void)solve;
         return sizeof(double) * ((size_t)KP_DOUBLES + (size_t)WAVES_PER_BLOCK * wsd);
     }
+    const bool f32 = solve && h->cfg.precision == ALIPMPC_PREC_FP32;
     int wsd = 0;
     switch (h->N) {
 #define WSCASE(NN)                                                                                     \
     case NN:                                                                                           \
-        wsd = solve ? wss_doubles<NN>(h->cfg.nc_max, h->cfg.ne_max, h->mr4_s, h->mo4)                  \
+        wsd = solve ? (f32 ? wss_elems<NN, float>(h->cfg.nc_max, h->cfg.ne_max, h->mr4_s, h->mo4)      \
+                           : wss_elems<NN, double>(h->cfg.nc_max, h->cfg.ne_max, h->mr4_s, h->mo4)) \
                     : ws_doubles<NN>(h->cfg.nc_max, h->cfg.ne_max, h->mr4);                            \
         break;
         WSCASE(1) WSCASE(2) WSCASE(3) WSCASE(4) WSCASE(5) WSCASE(6)
@@ -2900,7 +3134,9 @@ size_t smem_bytes(const Handle* h, bool solve)
     }
     const int e = solve ? ((h->NG * 5 + 3) & ~3) : h->NG * 5 + ((h->NG * 5) & 1);
     const int ncp = solve ? h->NCP : h->NCPU;
-    return sizeof(double) * ((size_t)KP_DOUBLES + (size_t)h->NG * ncp + e + (size_t)WAVES_PER_BLOCK * wsd);
+    // KP in fp64 units, then G, E and the per-wave workspaces in the kernel's arithmetic type
+    return sizeof(double) * (size_t)KP_DOUBLES +
+           (f32 ? sizeof(float) : sizeof(double)) * ((size_t)h->NG * ncp + e + (size_t)WAVES_PER_BLOCK * wsd);
 }
 
 KP make_kp(const Handle* h, long long B, bool solve)
@@ -2943,22 +3179,6 @@ KP make_kp(const Handle* h, long long B, bool solve)
     return P;
 }
 
-// dynamic-LDS opt-in, once per kernel and size (hipFuncSetAttribute is a host round trip: keep it out of the
-// steady-state launch path)
-void set_smem(const void* f, size_t smem)
-{
-    static std::mutex mtx;
-    static std::unordered_map<const void*, size_t> done[64];   // per device ordinal
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    std::lock_guard<std::mutex> lk(mtx);
-    auto& d = done[dev & 63];
-    auto it = d.find(f);
-    if (it != d.end() && it->second >= smem) return;
-    (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    d[f] = smem;
-}
-
 // J-layout steps (4 rows each) of the compiled solve kernels; mo4 is rounded up to 4 * ksm_of(rows)
 int ksm_of(int rows)
 {
@@ -2968,77 +3188,28 @@ int ksm_of(int rows)
     return 1 << 20;
 }
 
-template <int N>
-hipError_t launch_t(bool solve, const KP& P, size_t smem, hipStream_t st)
-{
-    const unsigned grid = (unsigned)((P.B + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
-    if (solve) {
-        // KSM = 4-row steps of the J layout, the smallest compiled size covering mo4 rows
-        auto go = [&](auto kern) {
-            set_smem((const void*)kern, smem);
-            hipLaunchKernelGGL(kern, dim3(grid), dim3(WAVE * WAVES_PER_BLOCK), smem, st, P);
-        };
-        if (P.mo4 <= 32)
-            go(solve_kernel<N, 8>);
-        else if (P.mo4 <= 40)
-            go(solve_kernel<N, 10>);
-        else if (P.mo4 <= 48)
-            go(solve_kernel<N, 12>);
-        else if (P.mo4 <= 64)
-            go(solve_kernel<N, 16>);
-        else if (P.mo4 <= 96)
-            go(solve_kernel<N, 24>);
-        else if (P.mo4 <= 128)
-            go(solve_kernel<N, 32>);
-        else
-            go(solve_kernel<N, 48>);
-    } else {
-        set_smem((const void*)eval_kernel<N>, smem);
-        hipLaunchKernelGGL(eval_kernel<N>, dim3(grid), dim3(WAVE * WAVES_PER_BLOCK), smem, st, P);
-    }
-    return hipGetLastError();
-}
-
-template <int N>
-hipError_t launch_dd(bool solve, const KP& P, size_t smem, hipStream_t st)
-{
-    const unsigned grid = (unsigned)((P.B + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
-    auto go = [&](auto kern) {
-        set_smem((const void*)kern, smem);
-        hipLaunchKernelGGL(kern, dim3(grid), dim3(WAVE * WAVES_PER_BLOCK), smem, st, P);
-    };
-    if (!solve)
-        go(dd_eval_kernel<N>);
-    else if (P.mo4 <= WAVE)
-        go(dd_solve_kernel<N, 1>);
-    else if (P.mo4 <= 2 * WAVE)
-        go(dd_solve_kernel<N, 2>);
-    else
-        go(dd_solve_kernel<N, 3>);
-    return hipGetLastError();
-}
-
 hipError_t launch(const Handle* h, bool solve, const KP& P, hipStream_t st)
 {
     const size_t smem = smem_bytes(h, solve);
+    const bool f32 = h->cfg.precision == ALIPMPC_PREC_FP32;
     if (h->cfg.variant == ALIPMPC_VARIANT_DD) {
         switch (h->N) {
-        case 1: return launch_dd<1>(solve, P, smem, st);
-        case 2: return launch_dd<2>(solve, P, smem, st);
-        case 3: return launch_dd<3>(solve, P, smem, st);
-        case 4: return launch_dd<4>(solve, P, smem, st);
-        case 5: return launch_dd<5>(solve, P, smem, st);
-        case 6: return launch_dd<6>(solve, P, smem, st);
+        case 1: return launch_dd_1(solve, P, smem, st);
+        case 2: return launch_dd_2(solve, P, smem, st);
+        case 3: return launch_dd_3(solve, P, smem, st);
+        case 4: return launch_dd_4(solve, P, smem, st);
+        case 5: return launch_dd_5(solve, P, smem, st);
+        case 6: return launch_dd_6(solve, P, smem, st);
         }
         return hipErrorInvalidValue;
     }
     switch (h->N) {
-    case 1: return launch_t<1>(solve, P, smem, st);
-    case 2: return launch_t<2>(solve, P, smem, st);
-    case 3: return launch_t<3>(solve, P, smem, st);
-    case 4: return launch_t<4>(solve, P, smem, st);
-    case 5: return launch_t<5>(solve, P, smem, st);
-    case 6: return launch_t<6>(solve, P, smem, st);
+    case 1: return launch_lip_1(solve, f32, P, smem, st);
+    case 2: return launch_lip_2(solve, f32, P, smem, st);
+    case 3: return launch_lip_3(solve, f32, P, smem, st);
+    case 4: return launch_lip_4(solve, f32, P, smem, st);
+    case 5: return launch_lip_5(solve, f32, P, smem, st);
+    case 6: return launch_lip_6(solve, f32, P, smem, st);
     }
     return hipErrorInvalidValue;
 }
@@ -3156,7 +3327,9 @@ int alipmpc_create(const alipmpc_cfg* cfg, int device, void** handle)
     if (cfg->N < 1 || cfg->N > ALIPMPC_MAX_N || cfg->nc_max < 0 || cfg->ne_max < 0 ||
         cfg->nc_max + cfg->ne_max > ALIPMPC_MAX_OBS || cfg->max_iter < 0 || cfg->max_iter > FILTER_CAP - 2)
         return ALIPMPC_EINVAL;
-    if (cfg->precision != ALIPMPC_PREC_FP64) return ALIPMPC_EUNSUPPORTED;
+    if (cfg->precision != ALIPMPC_PREC_FP64 && cfg->precision != ALIPMPC_PREC_FP32) return ALIPMPC_EINVAL;
+    // fp32 arithmetic is implemented for the LIP solve kernels (modi, sig_step)
+    if (cfg->precision == ALIPMPC_PREC_FP32 && cfg->variant == ALIPMPC_VARIANT_DD) return ALIPMPC_EUNSUPPORTED;
     if (cfg->variant != ALIPMPC_VARIANT_MODI && cfg->variant != ALIPMPC_VARIANT_SIG_STEP &&
         cfg->variant != ALIPMPC_VARIANT_DD)
         return ALIPMPC_EINVAL;
@@ -3527,3 +3700,4 @@ void alipmpc_destroy(void* handle)
 }
 
 }  // extern "C"
+#endif  // ALIP_PART_HOST
