@@ -6,7 +6,8 @@
 """
 from ._lib import (Cfg, Solver, default_cfg, load, lib_path, num_vars, rows_per_step, EXPORTS, STATUS_NAMES,
                    VARIANT_MODI, VARIANT_SIG_STEP, VARIANT_DD, PREC_FP64, PREC_FP32, ROLLOUT_DONE, FP32_TOL,
-                   FP32_ACCEPTABLE_TOL)
+                   FP32_ACCEPTABLE_TOL, FP32_TOL_LONG, FP32_ACCEPTABLE_TOL_LONG)
 
 __all__ = ["Cfg", "Solver", "default_cfg", "load", "lib_path", "num_vars", "rows_per_step", "EXPORTS",
-           "STATUS_NAMES", "VARIANT_MODI", "VARIANT_SIG_STEP", "VARIANT_DD", "PREC_FP64", "PREC_FP32", "ROLLOUT_DONE", "FP32_TOL", "FP32_ACCEPTABLE_TOL"]
+           "STATUS_NAMES", "VARIANT_MODI", "VARIANT_SIG_STEP", "VARIANT_DD", "PREC_FP64", "PREC_FP32", "ROLLOUT_DONE", "FP32_TOL", "FP32_ACCEPTABLE_TOL",
+           "FP32_TOL_LONG", "FP32_ACCEPTABLE_TOL_LONG"]

@@ -84,10 +84,13 @@ def load(build_if_missing=True):
 
 
 # fp32 solve kernels (cfg.precision = PREC_FP32, BASELINE cfg5): the fp64 tolerance 1e-8 is below fp32
-# resolution, so unless the caller sets them the fp32 tolerances are tol 1e-4 / acceptable 1e-3 (tools/
-# fp32_study.py: foothold within 1e-3 of the fp64 solve on 99.9 % of the instances both converge on, the
-# same feasible fraction, 1.5x the fp64 throughput).
+# resolution, so unless the caller sets them the fp32 tolerances are tol 1e-4 / acceptable 1e-3 for N <= 3
+# and 3e-4 / 3e-3 for longer horizons, whose decision-space gradients (through A^k) are larger and put the
+# fp32 stationarity floor higher.  tools/fp32_study.py (profiles/): N = 3 foothold within 1e-3 of the fp64
+# solve on 99.8 % of the instances both converge on, same feasible fraction, 1.5x the fp64 throughput;
+# N = 5 with ellipses 99 % within 1e-3, 1.7x.
 FP32_TOL, FP32_ACCEPTABLE_TOL = 1e-4, 1e-3
+FP32_TOL_LONG, FP32_ACCEPTABLE_TOL_LONG = 3e-4, 3e-3
 
 
 def default_cfg(variant=VARIANT_MODI, N=3, **overrides):
@@ -96,8 +99,9 @@ def default_cfg(variant=VARIANT_MODI, N=3, **overrides):
     if rc != 0:
         raise ValueError(f"alipmpc_default_cfg({variant}, {N}) -> {rc}")
     if overrides.get("precision") == PREC_FP32:
-        overrides.setdefault("tol", FP32_TOL)
-        overrides.setdefault("acceptable_tol", FP32_ACCEPTABLE_TOL)
+        long_h = N > 3
+        overrides.setdefault("tol", FP32_TOL_LONG if long_h else FP32_TOL)
+        overrides.setdefault("acceptable_tol", FP32_ACCEPTABLE_TOL_LONG if long_h else FP32_ACCEPTABLE_TOL)
     for k, v in overrides.items():
         if not hasattr(c, k):
             raise AttributeError(k)

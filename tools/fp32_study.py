@@ -30,6 +30,8 @@ def timed_solve(s, bt, B, N, reps=5):
     inp = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in bt.items() if v is not None}
     inp["leg"] = inp["leg"].to(torch.int8)
     inp["nc"] = inp["nc"].to(torch.int32)
+    if "ne" in inp:
+        inp["ne"] = inp["ne"].to(torch.int32)
     out = {"u": torch.empty((B, 5 * N), dtype=torch.float64, device=dev),
            "foot": torch.empty((B, 3), dtype=torch.float64, device=dev),
            "status": torch.empty(B, dtype=torch.int32, device=dev),
@@ -46,23 +48,25 @@ def timed_solve(s, bt, B, N, reps=5):
     return {k: v.cpu().numpy() for k, v in out.items()}, float(np.median(ts))
 
 
-def main(B=4096, N=3):
-    bt = scenes.make_batch(B, seed=0, n_cir=5, N=N)
-    base = alipmpc.default_cfg(0, N, nc_max=5, ne_max=0)
+def main(B=4096, N=3, n_elp=0, max_iter=30, tols=((1e-4, 1e-3), (3e-5, 1e-3), (1e-5, 1e-4), (1e-6, 1e-4))):
+    bt = scenes.make_batch_vec(B, seed=0, n_cir=5, n_elp=n_elp, N=N, fields=min(B, 1024))
+    kw = dict(nc_max=5, ne_max=n_elp, max_iter=max_iter)
+    base = alipmpc.default_cfg(0, N, **kw)
     s64 = alipmpc.Solver(base)
     o64, ms64 = timed_solve(s64, bt, B, N)
-    ev = s64.eval(bt["x0"], bt["goal"], bt["leg"], bt["cir"], bt["nc"], u=o64["u"], want_J=False)
+    ev = s64.eval(bt["x0"], bt["goal"], bt["leg"], bt["cir"], bt["nc"], bt["elp"], bt["ne"], u=o64["u"],
+                  want_J=False)
     v64 = violation(ev)
-    print(json.dumps(dict(prec="fp64", tol=base.tol, ms=ms64, iters_mean=float(o64["iters"].mean()),
+    print(json.dumps(dict(prec="fp64", N=N, n_elp=n_elp, max_iter=max_iter, tol=base.tol, ms=ms64, iters_mean=float(o64["iters"].mean()),
                           status={int(k): int(c) for k, c in zip(*np.unique(o64["status"], return_counts=True))},
                           feasible=float(np.mean(v64 <= 1e-4)))))
     ok64 = o64["status"] == 0
-    for tol, acc in [(1e-4, 1e-3), (3e-5, 1e-3), (1e-5, 1e-4), (1e-6, 1e-4)]:
-        cfg = alipmpc.default_cfg(0, N, nc_max=5, ne_max=0, precision=alipmpc.PREC_FP32, tol=tol,
-                                  acceptable_tol=acc)
+    for tol, acc in tols:
+        cfg = alipmpc.default_cfg(0, N, precision=alipmpc.PREC_FP32, tol=tol, acceptable_tol=acc, **kw)
         s32 = alipmpc.Solver(cfg)
         o32, ms32 = timed_solve(s32, bt, B, N)
-        ev = s64.eval(bt["x0"], bt["goal"], bt["leg"], bt["cir"], bt["nc"], u=o32["u"], want_J=False)
+        ev = s64.eval(bt["x0"], bt["goal"], bt["leg"], bt["cir"], bt["nc"], bt["elp"], bt["ne"], u=o32["u"],
+                      want_J=False)
         v32 = violation(ev)
         both = ok64 & (o32["status"] == 0)
         err = np.abs(o32["foot"] - o64["foot"]).max(axis=1)
@@ -79,3 +83,4 @@ def main(B=4096, N=3):
 
 if __name__ == "__main__":
     main()
+    main(B=4096, N=5, n_elp=5, max_iter=100, tols=((1e-3, 1e-2), (3e-4, 3e-3), (1e-4, 1e-3)))
