@@ -166,6 +166,8 @@ int alipmpc_eval_batch(void* handle, int64_t B,
  *   status_traj   B x S            solve status per step (ALIPMPC_ROLLOUT_DONE after the goal)
  *   iters_traj    B x S            interior-point iterations per step
  *   steps_to_goal B                steps taken until close_2_goal (-1: not within S)
+ *   u_traj        B x S x n        the plan (solution u) of every step (NaN after the goal); with x_traj it
+ *                                  feeds alipmpc_trace_batch for the per-step predicted traces
  * Host pointers when hip_stream == NULL, else device pointers (asynchronous; S solve launches + S small
  * plant-update launches on the stream, no host synchronisation).
  */
@@ -175,7 +177,23 @@ int alipmpc_rollout_batch(void* handle, int64_t B, int32_t S,
                           const double* elp, const int32_t* ne,
                           const double* u0, const double* last_u,
                           double* foot_traj, double* x_traj, int32_t* status_traj, int32_t* iters_traj,
-                          int32_t* steps_to_goal, void* hip_stream);
+                          int32_t* steps_to_goal, double* u_traj, void* hip_stream);
+
+/* Rows per planned step of alipmpc_trace_batch: 1 + len(np.arange(0, dt + 0.01, 0.01)) (42 at dt = 0.4);
+ * 0 for the DD variant. */
+int32_t alipmpc_trace_len(const alipmpc_cfg* cfg);
+
+/*
+ * Dense CoM traces of plans — the pos_det output of MPCCBF.gen_control_test (MPC_LIP_modi.py:117-122) built
+ * by MPCCBF.xk_track_det (MPC_LIP_modi.py:304-322), i.e. the 126 x 2 rows per plan of the reference's
+ * data_log *_pred_full_end.pkl at N = 3 (main_sim_mpc.py:117, logger_mpc.py:473).  For each instance and
+ * step k = 0..N-1: row 0 = x_k[0:2], then the ALIP flow from x_k around the stance foot p_k at t = 0, 0.01,
+ * ..., with x_{k+1} = M_A x_k + M_B u_k and p_k = W(u_k - A x_k) as gen_control_test forms them.
+ *   x0 B x 5, u B x 5N (a solve's u_out)  ->  trace B x N x alipmpc_trace_len(cfg) x 2.
+ * LIP variants only (DD: ALIPMPC_EUNSUPPORTED).  Host / device pointers as alipmpc_solve_batch.
+ */
+int alipmpc_trace_batch(void* handle, int64_t B, const double* x0, const double* u, double* trace,
+                        void* hip_stream);
 
 /* Duration in milliseconds of the most recent solve kernel launch on this handle, measured with HIP
  * events on the launch stream (0 if none). */

@@ -35,8 +35,8 @@ class Cfg(ctypes.Structure):
 
 
 EXPORTS = ("alipmpc_default_cfg", "alipmpc_rows_per_step", "alipmpc_num_vars", "alipmpc_create",
-           "alipmpc_solve_batch", "alipmpc_eval_batch", "alipmpc_rollout_batch", "alipmpc_last_kernel_ms", "alipmpc_last_error",
-           "alipmpc_destroy")
+           "alipmpc_solve_batch", "alipmpc_eval_batch", "alipmpc_rollout_batch", "alipmpc_trace_len",
+           "alipmpc_trace_batch", "alipmpc_last_kernel_ms", "alipmpc_last_error", "alipmpc_destroy")
 
 _lib = None
 
@@ -71,8 +71,12 @@ def load(build_if_missing=True):
     L.alipmpc_solve_batch.restype = ctypes.c_int
     L.alipmpc_eval_batch.argtypes = [P, ctypes.c_int64] + [P] * 18
     L.alipmpc_eval_batch.restype = ctypes.c_int
-    L.alipmpc_rollout_batch.argtypes = [P, ctypes.c_int64, ctypes.c_int32] + [P] * 15
+    L.alipmpc_rollout_batch.argtypes = [P, ctypes.c_int64, ctypes.c_int32] + [P] * 16
     L.alipmpc_rollout_batch.restype = ctypes.c_int
+    L.alipmpc_trace_len.argtypes = [ctypes.POINTER(Cfg)]
+    L.alipmpc_trace_len.restype = ctypes.c_int32
+    L.alipmpc_trace_batch.argtypes = [P, ctypes.c_int64, P, P, P, P]
+    L.alipmpc_trace_batch.restype = ctypes.c_int
     L.alipmpc_last_kernel_ms.argtypes = [P]
     L.alipmpc_last_kernel_ms.restype = ctypes.c_double
     L.alipmpc_last_error.argtypes = [P]
@@ -115,6 +119,10 @@ def rows_per_step(cfg):
 
 def num_vars(cfg):
     return int(load().alipmpc_num_vars(ctypes.byref(cfg)))
+
+
+def trace_len(cfg):
+    return int(load().alipmpc_trace_len(ctypes.byref(cfg)))
 
 
 STREAM_NULL = ctypes.c_void_p(ctypes.c_size_t(-1).value)   # ALIPMPC_STREAM_NULL
@@ -218,24 +226,35 @@ class Solver:
 
     def rollout(self, x0, goal, leg, cir, nc, elp=None, ne=None, u0=None, last_u=None, steps=8):
         """Closed-loop receding-horizon rollout (alipmpc_rollout_batch) from host arrays.  Returns
-        dict(foot (B,S,3), x (B,S+1,sdim), status (B,S), iters (B,S), steps_to_goal (B,))."""
+        dict(foot (B,S,3), x (B,S+1,sdim), status (B,S), iters (B,S), steps_to_goal (B,), u (B,S,n))."""
         B, x0, goal, leg, cir, nc, elp, ne = self._inputs(x0, goal, leg, cir, nc, elp, ne)
         u0 = np.ascontiguousarray(u0, np.float64).reshape(B, self.n)
         lu = None if last_u is None else np.ascontiguousarray(np.broadcast_to(np.asarray(last_u, np.float64), (B, 2)))
         S = int(steps)
         out = dict(foot=np.zeros((B, S, 3)), x=np.zeros((B, S + 1, self.sdim)), status=np.zeros((B, S), np.int32),
-                   iters=np.zeros((B, S), np.int32), steps_to_goal=np.zeros(B, np.int32))
+                   iters=np.zeros((B, S), np.int32), steps_to_goal=np.zeros(B, np.int32),
+                   u=np.zeros((B, S, self.n)))
         rc = self._L.alipmpc_rollout_batch(self._h, B, S, _ptr(x0), _ptr(goal), _ptr(leg), _ptr(cir), _ptr(nc),
                                            _ptr(elp), _ptr(ne), _ptr(u0), _ptr(lu), _ptr(out["foot"]),
                                            _ptr(out["x"]), _ptr(out["status"]), _ptr(out["iters"]),
-                                           _ptr(out["steps_to_goal"]), None)
+                                           _ptr(out["steps_to_goal"]), _ptr(out["u"]), None)
         self._check(rc, "alipmpc_rollout_batch")
+        return out
+
+    def trace(self, x0, u):
+        """Dense plan traces (alipmpc_trace_batch): x0 (B,5), u (B,5N) -> (B, N, trace_len, 2)."""
+        x0 = np.ascontiguousarray(x0, np.float64).reshape(-1, 5)
+        B = x0.shape[0]
+        u = np.ascontiguousarray(u, np.float64).reshape(B, self.n)
+        out = np.zeros((B, self.cfg.N, trace_len(self.cfg), 2))
+        rc = self._L.alipmpc_trace_batch(self._h, B, _ptr(x0), _ptr(u), _ptr(out), None)
+        self._check(rc, "alipmpc_trace_batch")
         return out
 
     # ---------------------------------------------------------------- device (torch) calls
     def rollout_device(self, inp, out, steps, stream=None):
         """Asynchronous rollout on device tensors: inp as solve_device, out dict with any of foot (B,S,3),
-        x (B,S+1,sdim), status (B,S), iters (B,S), steps_to_goal (B,)."""
+        x (B,S+1,sdim), status (B,S), iters (B,S), steps_to_goal (B,), u (B,S,n)."""
         import torch
         st = stream if stream is not None else torch.cuda.current_stream()
         B = inp["x0"].shape[0]
@@ -243,8 +262,15 @@ class Solver:
             self._h, B, int(steps), _ptr(inp["x0"]), _ptr(inp["goal"]), _ptr(inp.get("leg")), _ptr(inp["cir"]),
             _ptr(inp["nc"]), _ptr(inp.get("elp")), _ptr(inp.get("ne")), _ptr(inp["u0"]), _ptr(inp.get("last_u")),
             _ptr(out.get("foot")), _ptr(out.get("x")), _ptr(out.get("status")), _ptr(out.get("iters")),
-            _ptr(out.get("steps_to_goal")), _stream_arg(st))
+            _ptr(out.get("steps_to_goal")), _ptr(out.get("u")), _stream_arg(st))
         self._check(rc, "alipmpc_rollout_batch")
+
+    def trace_device(self, x0, u, trace, stream=None):
+        """Asynchronous dense plan traces on device tensors x0 (B,5), u (B,5N) -> trace (B,N,trace_len,2)."""
+        import torch
+        st = stream if stream is not None else torch.cuda.current_stream()
+        rc = self._L.alipmpc_trace_batch(self._h, x0.shape[0], _ptr(x0), _ptr(u), _ptr(trace), _stream_arg(st))
+        self._check(rc, "alipmpc_trace_batch")
 
     def solve_device(self, inp, out, stream=None):
         """Asynchronous solve on device tensors.  inp/out: dicts of torch CUDA tensors with the shapes of

@@ -51,6 +51,38 @@ def track_det(beta, xk, contr, t_rest):
     return np.concatenate([xk[None, 0:2], np.stack([px, py], 1)])
 
 
+def alip_constants(dt=0.4, g=9.81, H=1.0):
+    """MPCCBF.__init__ constants (MPC_LIP_modi.py:45-68): beta, A, B (B[4,2] = 1), W (a = 5, b = 1 weighted
+    pseudo-inverse), M_A = A - B W A, M_B = B W."""
+    beta = math.sqrt(g / H)
+    A, B = _alip_matrices(beta, dt, dt)
+    B[4, 2] = 1.0
+    ch, sh = math.cosh(beta * dt), math.sinh(beta * dt)
+    a, b = 5.0, 1.0
+    D = a * (ch - 1) ** 2 + b * (sh * beta) ** 2
+    Ch, Sh = -a * (ch - 1) / D, -b * sh * beta / D
+    W = np.array([[Ch, 0, Sh, 0, 0], [0, Ch, 0, Sh, 0], [0, 0, 0, 0, 1.0]])
+    return dict(beta=beta, A=A, B=B, W=W, M_A=A - B @ W @ A, M_B=B @ W)
+
+
+def plan_traces(beta, dt, A, W, M_A, M_B, x0s, us):
+    """numpy form of the pos_det traces of gen_control_test (MPC_LIP_modi.py:102-122) for many plans:
+    x0s (T,5), us (T,5N) -> (T, N, rows, 2) — what alipmpc_trace_batch computes on the device."""
+    x0s = np.asarray(x0s, float).reshape(-1, 5)
+    us = np.asarray(us, float).reshape(len(x0s), -1)
+    N = us.shape[1] // 5
+    out = []
+    for x0, u in zip(x0s, us):
+        xk, rows = x0, []
+        for i in range(N):
+            uk = u[5 * i:5 * (i + 1)]
+            pk = W @ (uk - A @ xk)
+            rows.append(track_det(beta, xk, pk, dt))
+            xk = M_A @ xk + M_B @ uk
+        out.append(np.stack(rows))
+    return np.stack(out) if out else np.zeros((0, N, 0, 2))
+
+
 class _Base:
     variant = _lib.VARIANT_MODI
 
@@ -63,16 +95,8 @@ class _Base:
         self.step_gap = 0.3
         # sigma = beta * coth(dt * beta / 2)   (MPC_LIP_modi.py:45)
         self.sigma = self.beta / math.tanh(self.dt * self.beta / 2)
-        A, B = _alip_matrices(self.beta, self.dt, self.dt)
-        B[4, 2] = 1.0
-        self.A, self.B = A, B
-        ch, sh = math.cosh(self.beta * self.dt), math.sinh(self.beta * self.dt)
-        a, b = 5.0, 1.0
-        D = a * (ch - 1) ** 2 + b * (sh * self.beta) ** 2
-        Ch, Sh = -a * (ch - 1) / D, -b * sh * self.beta / D
-        self.W = np.array([[Ch, 0, Sh, 0, 0], [0, Ch, 0, Sh, 0], [0, 0, 0, 0, 1.0]])
-        self.M_A = self.A - self.B @ self.W @ self.A
-        self.M_B = self.B @ self.W
+        k = alip_constants(self.dt)
+        self.A, self.B, self.W, self.M_A, self.M_B = k["A"], k["B"], k["W"], k["M_A"], k["M_B"]
         self.B_vel_shr = self.B[2:4, 0:2]
         self.inv_B_vel_shr = np.linalg.inv(self.B_vel_shr)
         self.cfg = _lib.default_cfg(self.variant, step, nc_max=max(nc_max, 0), ne_max=max(ne_max, 0),
@@ -91,6 +115,12 @@ class _Base:
 
     def xk_track_det(self, xk, contr, t_rest):
         return track_det(self.beta, xk, contr, t_rest)
+
+    def plan_traces(self, x0s, us, device=True):
+        """pos_det traces of many plans: on the GPU (alipmpc_trace_batch) or with numpy (device=False)."""
+        if device:
+            return self.solver.trace(x0s, us)
+        return plan_traces(self.beta, self.dt, self.A, self.W, self.M_A, self.M_B, x0s, us)
 
     def alip_des_vel(self, vx_max, leg_ind):
         vdes_x = self.sigma * vx_max * self.dt / 2

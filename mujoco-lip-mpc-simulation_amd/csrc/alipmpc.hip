@@ -2797,6 +2797,7 @@ struct AdvP {
     int32_t* status_traj;  // B x S
     int32_t* iters_traj;   // B x S
     int32_t* steps_to_goal;  // B
+    double* u_traj;        // B x S x n   the plan of every step (NaN after the goal)
 };
 
 __global__ __launch_bounds__(256) void advance_kernel(AdvP A)
@@ -2811,6 +2812,8 @@ __global__ __launch_bounds__(256) void advance_kernel(AdvP A)
             for (int i = 0; i < sd; ++i) A.x_traj[((size_t)b * (S + 1) + t + 1) * sd + i] = A.x[(size_t)b * sd + i];
         if (A.status_traj) A.status_traj[(size_t)b * S + t] = ALIPMPC_ROLLOUT_DONE;
         if (A.iters_traj) A.iters_traj[(size_t)b * S + t] = 0;
+        if (A.u_traj)
+            for (int i = 0; i < n; ++i) A.u_traj[((size_t)b * S + t) * n + i] = NAN;
         return;
     }
     const double* xp = A.x_pred + (size_t)b * N * sd;
@@ -2824,6 +2827,8 @@ __global__ __launch_bounds__(256) void advance_kernel(AdvP A)
     }
     const double* ub = A.u + (size_t)b * n;
     double* u0 = A.u0 + (size_t)b * n;
+    if (A.u_traj)
+        for (int i = 0; i < n; ++i) A.u_traj[((size_t)b * S + t) * n + i] = ub[i];
     if (A.variant == ALIPMPC_VARIANT_SIG_STEP) {
         const int blk = n / N;
         for (int k = 0; k < N; ++k) {
@@ -2862,6 +2867,64 @@ __global__ __launch_bounds__(256) void rollout_init_kernel(long long B, int S, i
     if (steps_to_goal) steps_to_goal[b] = -1;
     if (xtraj)
         for (int i = 0; i < sd; ++i) xtraj[(size_t)b * (S + 1) * sd + i] = x0[(size_t)b * sd + i];
+}
+
+// ------------------------------------------------------------------------------------------------
+// dense CoM traces of a plan (the pos_det output of MPCCBF.gen_control_test, MPC_LIP_modi.py:117-122,
+// 304-322): for step k, rows [x_k[0:2]; pos(t_i)], t_i = i * 0.01 (np.arange(0, dt + 0.01, 0.01)), of the
+// continuous ALIP flow from x_k around the stance foot p_k:  pos(t) = ch x_k[0:2] + sh/beta x_k[2:4] +
+// (1 - ch) p_k[0:2].  x_{k+1} = M_A x_k + M_B u_k and p_k = W (u_k - A x_k) as gen_control_test forms them.
+// One thread per output row (coalesced 16-byte stores); HBM-bound: 40 B of plan in, rows x 16 B out.
+// ------------------------------------------------------------------------------------------------
+struct TrP {
+    long long B;
+    int N, rows;        // rows per step = 1 + samples
+    double beta, step;  // sample spacing 0.01
+    double A[25], W[15], MA[25], MB[25];
+    const double* x0;   // B x 5
+    const double* u;    // B x 5N
+    double* trace;      // B x N x rows x 2
+};
+
+__global__ __launch_bounds__(256) void trace_kernel(TrP T)
+{
+    const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long per = (long long)T.N * T.rows;
+    if (gid >= T.B * per) return;
+    const long long b = gid / per;
+    const int rem = (int)(gid - b * per), k = rem / T.rows, r = rem - k * T.rows;
+    const double* ub = T.u + (size_t)b * 5 * T.N;
+    double x[5];
+    for (int i = 0; i < 5; ++i) x[i] = T.x0[(size_t)b * 5 + i];
+    for (int j = 0; j < k; ++j) {   // x_{j+1} = M_A x_j + M_B u_j
+        double y[5];
+        for (int i = 0; i < 5; ++i) {
+            double v = 0.0;
+            for (int c = 0; c < 5; ++c) v += T.MA[i * 5 + c] * x[c];
+            for (int c = 0; c < 5; ++c) v += T.MB[i * 5 + c] * ub[5 * j + c];
+            y[i] = v;
+        }
+        for (int i = 0; i < 5; ++i) x[i] = y[i];
+    }
+    double px = x[0], py = x[1];
+    if (r > 0) {
+        double ax[5], p[2];
+        for (int i = 0; i < 5; ++i) {
+            double v = 0.0;
+            for (int c = 0; c < 5; ++c) v += T.A[i * 5 + c] * x[c];
+            ax[i] = ub[5 * k + i] - v;
+        }
+        for (int i = 0; i < 2; ++i) {
+            double v = 0.0;
+            for (int c = 0; c < 5; ++c) v += T.W[i * 5 + c] * ax[c];
+            p[i] = v;
+        }
+        const double t = (r - 1) * T.step;
+        const double ch = cosh(T.beta * t), sh = sinh(T.beta * t);
+        px = ch * x[0] + sh / T.beta * x[2] + (1 - ch) * p[0];
+        py = ch * x[1] + sh / T.beta * x[3] + (1 - ch) * p[1];
+    }
+    reinterpret_cast<double2*>(T.trace)[gid] = make_double2(px, py);
 }
 #endif  // ALIP_PART_HOST
 
@@ -3535,7 +3598,7 @@ int alipmpc_eval_batch(void* handle, int64_t B, const double* x0, const double* 
 int alipmpc_rollout_batch(void* handle, int64_t B, int32_t S, const double* x0, const double* goal, const int8_t* leg,
                           const double* cir, const int32_t* nc, const double* elp, const int32_t* ne, const double* u0,
                           const double* last_u, double* foot_traj, double* x_traj, int32_t* status_traj,
-                          int32_t* iters_traj, int32_t* steps_to_goal, void* hip_stream)
+                          int32_t* iters_traj, int32_t* steps_to_goal, double* u_traj, void* hip_stream)
 {
     Handle* h = (Handle*)handle;
     if (!h) return ALIPMPC_EINVAL;
@@ -3557,7 +3620,7 @@ int alipmpc_rollout_batch(void* handle, int64_t B, int32_t S, const double* x0, 
             int8_t* leg;
             int32_t *st, *it;
             uint8_t* act;
-            double *goal, *cir, *elp, *ft, *xt;
+            double *goal, *cir, *elp, *ft, *xt, *ut;
             int32_t *nc, *ne, *stt, *itt, *sg;
         } l{};
         l.x = cv.take<double>(Bz * sd); l.u0 = cv.take<double>(Bz * n); l.lu = cv.take<double>(Bz * 2);
@@ -3569,6 +3632,7 @@ int alipmpc_rollout_batch(void* handle, int64_t B, int32_t S, const double* x0, 
             l.elp = cv.take<double>(Bz * 5 * cf.ne_max); l.nc = cv.take<int32_t>(Bz); l.ne = cv.take<int32_t>(Bz);
             l.ft = cv.take<double>(Bz * Sz * 3); l.xt = cv.take<double>(Bz * (Sz + 1) * sd);
             l.stt = cv.take<int32_t>(Bz * Sz); l.itt = cv.take<int32_t>(Bz * Sz); l.sg = cv.take<int32_t>(Bz);
+            if (u_traj) l.ut = cv.take<double>(Bz * Sz * n);
         }
         return l;
     };
@@ -3597,7 +3661,7 @@ int alipmpc_rollout_batch(void* handle, int64_t B, int32_t S, const double* x0, 
         HIPCHK(h, hipMemsetAsync(l.lu, 0, Bz * 2 * 8, st));
     const double *d_goal = goal, *d_cir = cir, *d_elp = elp;
     const int32_t *d_nc = nc, *d_ne = ne;
-    double *d_ft = foot_traj, *d_xt = x_traj;
+    double *d_ft = foot_traj, *d_xt = x_traj, *d_ut = u_traj;
     int32_t *d_stt = status_traj, *d_itt = iters_traj, *d_sg = steps_to_goal;
     if (host) {
         HIPCHK(h, hipMemcpyAsync(l.goal, goal, Bz * 2 * 8, hipMemcpyHostToDevice, st));
@@ -3613,6 +3677,7 @@ int alipmpc_rollout_batch(void* handle, int64_t B, int32_t S, const double* x0, 
         d_ft = foot_traj ? l.ft : nullptr; d_xt = x_traj ? l.xt : nullptr;
         d_stt = status_traj ? l.stt : nullptr; d_itt = iters_traj ? l.itt : nullptr;
         d_sg = steps_to_goal ? l.sg : nullptr;
+        d_ut = u_traj ? l.ut : nullptr;
     }
     const unsigned g1 = (unsigned)((B + 255) / 256);
     hipLaunchKernelGGL(rollout_init_kernel, dim3(g1), dim3(256), 0, st, (long long)B, (int)S, sd, (const double*)l.x,
@@ -3628,6 +3693,7 @@ int alipmpc_rollout_batch(void* handle, int64_t B, int32_t S, const double* x0, 
     A.x = l.x; A.u0 = l.u0; A.leg = l.leg; A.last_u = l.lu; A.u = l.u; A.foot = l.foot; A.x_pred = l.xp;
     A.status = l.st; A.iters = l.it; A.active = l.act;
     A.foot_traj = d_ft; A.x_traj = d_xt; A.status_traj = d_stt; A.iters_traj = d_itt; A.steps_to_goal = d_sg;
+    A.u_traj = d_ut;
     const int ei = h->evi;
     h->evi = (ei + 1) % Handle::NEV;
     HIPCHK(h, hipEventRecord(h->ev[ei][0], st));
@@ -3646,6 +3712,70 @@ int alipmpc_rollout_batch(void* handle, int64_t B, int32_t S, const double* x0, 
         if (status_traj) HIPCHK(h, hipMemcpyAsync(status_traj, l.stt, Bz * Sz * 4, hipMemcpyDeviceToHost, st));
         if (iters_traj) HIPCHK(h, hipMemcpyAsync(iters_traj, l.itt, Bz * Sz * 4, hipMemcpyDeviceToHost, st));
         if (steps_to_goal) HIPCHK(h, hipMemcpyAsync(steps_to_goal, l.sg, Bz * 4, hipMemcpyDeviceToHost, st));
+        if (u_traj) HIPCHK(h, hipMemcpyAsync(u_traj, l.ut, Bz * Sz * n * 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(h, hipStreamSynchronize(st));
+    }
+    return ALIPMPC_OK;
+}
+
+int32_t alipmpc_trace_len(const alipmpc_cfg* cfg)
+{
+    if (!cfg || cfg->variant == ALIPMPC_VARIANT_DD || !(cfg->dt > 0)) return 0;
+    // numpy arange length: ceil((stop - start) / step) with stop = dt + 0.01, step = 0.01; + the x_k row
+    return 1 + (int32_t)std::ceil((cfg->dt + 0.01) / 0.01);
+}
+
+int alipmpc_trace_batch(void* handle, int64_t B, const double* x0, const double* u, double* trace, void* hip_stream)
+{
+    Handle* h = (Handle*)handle;
+    if (!h) return ALIPMPC_EINVAL;
+    const alipmpc_cfg& cf = h->cfg;
+    if (cf.variant == ALIPMPC_VARIANT_DD) return fail(h, ALIPMPC_EUNSUPPORTED, "trace: LIP variants only");
+    if (B < 0) return fail(h, ALIPMPC_EINVAL, "B < 0");
+    if (B == 0) return ALIPMPC_OK;
+    if (!x0 || !u || !trace) return fail(h, ALIPMPC_EINVAL, "missing pointer");
+    HIPCHK(h, hipSetDevice(h->device));
+    const int N = h->N, rows = alipmpc_trace_len(&cf);
+    const size_t Bz = (size_t)B, nout = Bz * N * rows * 2;
+    TrP T;
+    std::memset(&T, 0, sizeof(T));
+    T.B = B; T.N = N; T.rows = rows; T.step = 0.01;
+    T.beta = std::sqrt(cf.g / cf.H);
+    {
+        const double b = T.beta, dT = cf.dt, ch = std::cosh(b * dT), sh = std::sinh(b * dT);
+        const double A[25] = {ch, 0, sh / b, 0, 0, 0, ch, 0, sh / b, 0, sh * b, 0, ch, 0, 0,
+                              0, sh * b, 0, ch, 0, 0, 0, 0, 0, 1};
+        const double Bm[15] = {1 - ch, 0, 0, 0, 1 - ch, 0, -sh * b, 0, 0, 0, -sh * b, 0, 0, 0, 1};
+        const double Dd = 5.0 * (ch - 1) * (ch - 1) + (sh * b) * (sh * b);
+        const double Ch = -5.0 * (ch - 1) / Dd, Sh = -sh * b / Dd;
+        const double W[15] = {Ch, 0, Sh, 0, 0, 0, Ch, 0, Sh, 0, 0, 0, 0, 0, 1};
+        double BWA[25];
+        std::memcpy(T.A, A, sizeof(A));
+        std::memcpy(T.W, W, sizeof(W));
+        mm(Bm, W, T.MB, 5, 3, 5);
+        mm(T.MB, A, BWA, 5, 5, 5);
+        for (int i = 0; i < 25; ++i) T.MA[i] = A[i] - BWA[i];
+    }
+    hipStream_t st = stream_of(h, hip_stream);
+    const bool host = hip_stream == nullptr;
+    if (host) {
+        const size_t bytes = Bz * 5 * 8 + Bz * 5 * N * 8 + nout * 8 + 512;
+        if (int rc = ensure_stage(h, bytes)) return rc;
+        Carver cv{(char*)h->stage};
+        double* dx = cv.take<double>(Bz * 5);
+        double* du = cv.take<double>(Bz * 5 * N);
+        double* dt_ = cv.take<double>(nout);
+        HIPCHK(h, hipMemcpyAsync(dx, x0, Bz * 5 * 8, hipMemcpyHostToDevice, st));
+        HIPCHK(h, hipMemcpyAsync(du, u, Bz * 5 * N * 8, hipMemcpyHostToDevice, st));
+        T.x0 = dx; T.u = du; T.trace = dt_;
+    } else {
+        T.x0 = x0; T.u = u; T.trace = trace;
+    }
+    const long long total = (long long)B * N * rows;
+    hipLaunchKernelGGL(trace_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, T);
+    HIPCHK(h, hipGetLastError());
+    if (host) {
+        HIPCHK(h, hipMemcpyAsync(trace, T.trace, nout * 8, hipMemcpyDeviceToHost, st));
         HIPCHK(h, hipStreamSynchronize(st));
     }
     return ALIPMPC_OK;

@@ -192,6 +192,7 @@ def rollout_batch(cfg, x0, goal, leg, cir, nc, elp, ne, u0, last_u=None, steps=8
     status = np.full((B, S), -10, np.int32)
     iters = np.zeros((B, S), np.int32)
     stg = np.full(B, -1, np.int32)
+    uts = np.full((B, S, n), np.nan)
     active = np.ones(B, bool)
     elp_a = None if elp is None else np.asarray(elp)
     ne_a = None if ne is None else np.asarray(ne)
@@ -211,6 +212,7 @@ def rollout_batch(cfg, x0, goal, leg, cir, nc, elp, ne, u0, last_u=None, steps=8
             xp = o["x_pred"]
             x[idx] = xp[:, 0]
             u = o["u"]
+            uts[idx, t] = u
             if cfg.variant == VARIANT_SIG_STEP:
                 blk = n // N
                 ub = u.reshape(len(idx), N, blk)
@@ -230,4 +232,4 @@ def rollout_batch(cfg, x0, goal, leg, cir, nc, elp, ne, u0, last_u=None, steps=8
             active[done] = False
             stg[done] = t + 1
         xs[:, t + 1] = x
-    return dict(foot=foot, x=xs, status=status, iters=iters, steps_to_goal=stg)
+    return dict(foot=foot, x=xs, status=status, iters=iters, steps_to_goal=stg, u=uts)

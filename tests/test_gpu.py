@@ -411,3 +411,58 @@ def test_fp32_dd_unsupported(gpu_lib):
     cfg = gpu_lib.default_cfg(gpu_lib.VARIANT_DD, 3, precision=gpu_lib.PREC_FP32)
     with pytest.raises(RuntimeError, match="EUNSUPPORTED"):
         gpu_lib.Solver(cfg)
+
+
+@pytest.mark.parametrize("variant,N", [(0, 3), (1, 3), (0, 5)])
+def test_trace_batch_matches_plan_traces(gpu_lib, variant, N):
+    """alipmpc_trace_batch (trace_kernel) against the numpy restatement of gen_control_test's pos_det
+    (planner.plan_traces = xk_track_det per planned step, pinned to the reference by g4_aux), on solve
+    outputs; host and device pointer paths."""
+    from alipmpc import planner, scenes
+    bt = scenes.make_batch(200, seed=61 + N, n_cir=5, N=N)
+    cfg = gpu_lib.default_cfg(variant, N, nc_max=5, ne_max=0)
+    s = gpu_lib.Solver(cfg)
+    o = s.solve(bt["x0"], bt["goal"], bt["leg"], bt["cir"], bt["nc"], u0=bt["u0"])
+    tr = s.trace(bt["x0"], o["u"])
+    assert tr.shape == (200, N, 42, 2)
+    k = planner.alip_constants()
+    ref = planner.plan_traces(k["beta"], 0.4, k["A"], k["W"], k["M_A"], k["M_B"], bt["x0"], o["u"])
+    assert np.max(np.abs(tr - ref)) < 1e-12
+    import torch
+    dev = torch.device("cuda", 0)
+    td = torch.empty((200, N, 42, 2), dtype=torch.float64, device=dev)
+    s.trace_device(torch.from_numpy(bt["x0"]).to(dev), torch.from_numpy(o["u"]).to(dev), td)
+    torch.cuda.synchronize()
+    assert np.array_equal(td.cpu().numpy(), tr)
+    with pytest.raises(RuntimeError, match="EUNSUPPORTED"):
+        gpu_lib.Solver(gpu_lib.default_cfg(gpu_lib.VARIANT_DD, 3)).trace(bt["x0"][:, :5], np.zeros((200, 15)))
+
+
+def test_rollout_plans_and_data_log(gpu_lib, coracle, tmp_path):
+    """rollout u_traj (the plan of every step) is consistent with the executed steps, and data_log episode
+    logs built from the GPU rollout + GPU traces equal those built with the numpy traces."""
+    from alipmpc import datalog, planner, scenes
+    B, S = 64, 6
+    bt = scenes.make_batch(B, seed=77, n_cir=5)
+    x0 = bt["x0"].copy()
+    x0[:8, 0:2] = bt["goal"][:8] - np.array([0.4, 0.3])
+    s = gpu_lib.Solver(gpu_lib.default_cfg(0, 3, nc_max=5, ne_max=0))
+    r = s.rollout(x0, bt["goal"], bt["leg"], bt["cir"], bt["nc"], u0=np.tile(x0, (1, 3)), steps=S)
+    act = r["status"] != gpu_lib.ROLLOUT_DONE
+    assert np.array_equal(r["u"][:, :, 0:5][act], r["x"][:, 1:][act])      # x^(t+1) = plan's x_1
+    assert np.isnan(r["u"][~act]).all()
+    assert np.array_equal(r["u"][:, :, 0:3][act] * 0 + 1, np.ones_like(r["u"][:, :, 0:3][act]))
+    k = planner.alip_constants()
+    for b in (0, 1, 9, 20):
+        lg = datalog.episode_logs(r, b, s.trace, cir=bt["cir"][b])
+        ln = datalog.episode_logs(r, b, lambda xs, us: planner.plan_traces(k["beta"], 0.4, k["A"], k["W"],
+                                                                         k["M_A"], k["M_B"], xs, us),
+                                  cir=bt["cir"][b])
+        for name in datalog.NAMES:
+            a, c = lg[name], ln[name]
+            if isinstance(c, list):
+                assert len(a) == len(c) and all(np.max(np.abs(x - y), initial=0) < 1e-12 for x, y in zip(a, c))
+            else:
+                assert np.max(np.abs(np.asarray(a) - np.asarray(c)), initial=0) < 1e-12, name
+        datalog.write_data_log(str(tmp_path / f"LIP_gpu{b}_"), lg)
+    assert (r["steps_to_goal"][:8] > 0).sum() >= 4
