@@ -76,3 +76,31 @@ def test_episode_logs_roundtrip(coracle, tmp_path):
             else:
                 assert np.array_equal(np.asarray(a), np.asarray(r))
     assert (roll["steps_to_goal"][0] > 0)
+
+
+def test_tsc_command_packing_matches_reference(golden):
+    """Batched planner -> TSC command helpers against the reference Logger (logger_mpc.py), golden g5."""
+    from alipmpc import tsc
+    g = golden("g5_logger")
+    assert np.max(np.abs(tsc.angle_a_minus_b(g["amb_in"][:, 0], g["amb_in"][:, 1]) - g["amb_out"])) < 1e-15
+    assert np.max(np.abs(tsc.tube_step(g["tube_in"][:, 0], g["tube_in"][:, 1]) - g["tube_out"])) < 1e-15
+    a = g["avg_in"]
+    assert np.max(np.abs(tsc.avg_hd(a[:, 0], a[:, 1], a[:, 2:5]) - g["avg_out"])) < 1e-15
+    assert np.max(np.abs(tsc.map_to_robot_pos(g["frame_in"], [0.3, -0.2], 0.25) - g["pos_m2r"])) < 1e-14
+    assert np.max(np.abs(tsc.map_to_robot_vel(g["frame_in"], 0.25) - g["vel_m2r"])) < 1e-14
+    t = g["tsc_in"]
+    out = tsc.gen_tsc_control(t[:, 0:2], t[:, 2:4], t[:, 4:6], t[:, 6], t[:, 7], t[:, 8], t[:, 9])
+    assert out.shape == (16, 8) and np.max(np.abs(out - g["tsc_out"])) < 1e-15
+
+
+def test_foot_frame_inputs_geometry():
+    from alipmpc import tsc
+    rng = np.random.default_rng(4)
+    nex, cur, pos, vel = (rng.normal(size=(10, 2)) for _ in range(4))
+    ang = rng.uniform(-3, 3, 10)
+    fi, npf, nvf = tsc.foot_frame_inputs(nex, cur, ang, pos, vel)
+    for b in range(10):
+        M_T = np.array([[np.cos(ang[b]), np.sin(ang[b])], [-np.sin(ang[b]), np.cos(ang[b])]])
+        assert np.allclose(fi[b], M_T @ (nex[b] - cur[b]), rtol=0, atol=1e-15)
+        assert np.allclose(npf[b], M_T @ (pos[b] - cur[b]), rtol=0, atol=1e-15)
+        assert np.allclose(nvf[b], M_T @ vel[b], rtol=0, atol=1e-15)

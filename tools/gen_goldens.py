@@ -567,6 +567,53 @@ def gen_g4(modi, sig):
     print("g4 aux written")
 
 
+def gen_g5_logger():
+    """Caller-side helpers of the planner -> controller interface in data_procs/logger_mpc.py (Logger):
+    angle_A_minus_B (:169-175), tube_func (:283-300), avg_hd (:208-215), the frame transforms
+    pos/vel_map_glo_2_robo_glo (:134-150), the foot-frame inputs of gen_nex_foot_input (:349-360, inline
+    code: restated on the same attributes) and gen_tsc_control (:374-384)."""
+    import contextlib
+    import io
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("ref_logger_mpc", os.path.join(REF, "data_procs", "logger_mpc.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    rng = np.random.default_rng(123)
+    R = {}
+    lg = mod.Logger(0.4, [0.3, -0.2], 0.25, [[10, 10]], [-0.5, 10.5])
+    ab = rng.uniform(-7, 7, (40, 2))
+    R["amb_in"] = ab
+    R["amb_out"] = np.array([lg.angle_A_minus_B(a, b) for a, b in ab])
+    tin = np.concatenate([rng.uniform(-0.4, 0.4, (30, 2)), [[0.0, 0.3], [0.15, 0.1], [-0.15, 0.2]]])
+    R["tube_in"] = tin
+    with contextlib.redirect_stdout(io.StringIO()):
+        R["tube_out"] = np.array([lg.tube_func(t, v) for t, v in tin])
+    av_in, av_out = [], []
+    for _ in range(20):
+        cur, turn = rng.uniform(-3, 3), rng.uniform(-0.2, 0.2)
+        hds = rng.uniform(-3.5, 3.5, 3)
+        lg.nex_turn = turn
+        lg.mpc_hds_list = list(hds)
+        av_in.append([cur, turn, *hds]); av_out.append(lg.avg_hd(cur))
+    R["avg_in"] = np.array(av_in); R["avg_out"] = np.array(av_out)
+    pv = rng.normal(0, 3, (12, 2))
+    R["frame_in"] = pv
+    R["pos_m2r"] = np.array([lg.pos_map_glo_2_robo_glo(v) for v in pv])
+    R["vel_m2r"] = np.array([lg.vel_map_glo_2_robo_glo(v) for v in pv])
+    ts_in, ts_out = [], []
+    for t in range(16):
+        lg.foot_input = rng.normal(0, 0.3, 2); lg.nex_pos_fot_loc = rng.normal(0, 0.2, 2)
+        lg.nex_vel_fot_loc = rng.normal(0, 0.5, 2); lg.hd_input_pr = rng.uniform(-0.3, 0.3)
+        lg.hd_input_cos = rng.uniform(-3, 3)
+        i, n_cyc = int(rng.integers(0, 40)), 40
+        ts_in.append([*lg.foot_input, *lg.nex_pos_fot_loc, *lg.nex_vel_fot_loc, lg.hd_input_pr, lg.hd_input_cos, i,
+                      n_cyc])
+        ts_out.append(lg.gen_tsc_control(i, n_cyc))
+    R["tsc_in"] = np.array(ts_in); R["tsc_out"] = np.array(ts_out)
+    np.savez_compressed(os.path.join(OUT, "g5_logger.npz"), **R)
+    print("g5 logger written")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
@@ -584,6 +631,8 @@ def main():
         gen_g2(modi, sig, rand_obs, 24 if a.quick else 64)
     if not only or "g4" in only:
         gen_g4(modi, sig)
+    if not only or "g5" in only:
+        gen_g5_logger()
     if not only or "g3s" in only:
         gen_g3_sup_learn(modi, a.quick)
     if not only or "g3y" in only:
