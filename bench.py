@@ -106,8 +106,11 @@ def main():
         B = args.batch
     elif preset["per_gpu"]:
         B = preset["batch"]
-    else:   # a fixed total sharded over the ranks (contiguous shards; the last rank takes the remainder)
-        B = preset["batch"] // world + (preset["batch"] % world if rank == world - 1 else 0)
+    else:   # a fixed total sharded over the ranks (contiguous shards, sizes differ by at most one)
+        from alipmpc import sharding
+        lo, hi = sharding.shard_range(preset["batch"], rank, world)
+        B = hi - lo
+    B_cap = -(-preset["batch"] // world) if not (preset["per_gpu"] or args.batch is not None) else B
     prec = {"precision": alipmpc.PREC_FP32} if fp32 else {}
     cfg = alipmpc.default_cfg(variant, N, nc_max=n_cir, ne_max=n_elp, **prec)
     solver = alipmpc.Solver(cfg, device=dev.index)
@@ -137,19 +140,23 @@ def main():
         "iters": torch.empty((B,), dtype=torch.int32, device=dev),
     }
     # one gather of per-instance outputs (u, foot, status, iters packed as fp64 rows) to rank 0
+    # (padded to the largest shard so every rank contributes the same shape)
     pack_w = n + 3 + 2
-    packed = torch.empty((B, pack_w), dtype=torch.float64, device=dev)
+    packed = torch.zeros((B_cap, pack_w), dtype=torch.float64, device=dev)
     gathered = [torch.empty_like(packed) for _ in range(world)] if (world > 1 and rank == 0) else None
     stream = torch.cuda.current_stream(dev)
+
+    def pack_and_gather():
+        packed[:B, :n] = out["u"]
+        packed[:B, n:n + 3] = out["foot"]
+        packed[:B, n + 3] = out["status"].to(torch.float64)
+        packed[:B, n + 4] = out["iters"].to(torch.float64)
+        dist.gather(packed, gathered, dst=0)
 
     def step():
         solver.solve_device(inp, out, stream=stream)
         if world > 1:
-            packed[:, :n] = out["u"]
-            packed[:, n:n + 3] = out["foot"]
-            packed[:, n + 3] = out["status"].to(torch.float64)
-            packed[:, n + 4] = out["iters"].to(torch.float64)
-            dist.gather(packed, gathered, dst=0)
+            pack_and_gather()
 
     for _ in range(args.warmup):
         step()
@@ -165,11 +172,7 @@ def main():
         solver.solve_device(inp, out, stream=stream)
         ev[k][1].record(stream)
         if world > 1:
-            packed[:, :n] = out["u"]
-            packed[:, n:n + 3] = out["foot"]
-            packed[:, n + 3] = out["status"].to(torch.float64)
-            packed[:, n + 4] = out["iters"].to(torch.float64)
-            dist.gather(packed, gathered, dst=0)
+            pack_and_gather()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()

@@ -42,25 +42,35 @@ def _run(cmd, verbose):
     subprocess.check_call(cmd)
 
 
-def build(force=False, verbose=True, extra=()):
-    if not force and not needs_build():
+def build(force=False, verbose=True, extra=(), out=None, src=None):
+    """Build the library (out / src: output path and source of dev variants, e.g. extra=["-DALIP_STAMPS"])."""
+    target = out or LIB
+    src = src or SRC
+    if not force and out is None and not needs_build():
         return LIB
-    tmp_lib = LIB + ".tmp"
+    tmp_lib = target + ".tmp"
     if os.environ.get("ALIPMPC_SINGLE_TU") == "1":
-        _run([HIPCC, *ARCH, *FLAGS, *extra, "-shared", "-o", tmp_lib, SRC], verbose)
+        _run([HIPCC, *ARCH, *FLAGS, *extra, "-shared", "-o", tmp_lib, src], verbose)
     else:
         jobs = max(1, min(len(PARTS), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1))))
         with tempfile.TemporaryDirectory(prefix="alipmpc_build_") as td:
             objs = [os.path.join(td, f"part{k}.o") for k in PARTS]
-            cmds = [[HIPCC, *ARCH, *FLAGS, *extra, f"-DALIP_PART={k}", "-c", "-o", o, SRC]
+            cmds = [[HIPCC, *ARCH, *FLAGS, *extra, f"-DALIP_PART={k}", "-c", "-o", o, src]
                     for k, o in zip(PARTS, objs)]
             with ThreadPoolExecutor(jobs) as ex:
                 for f in [ex.submit(_run, c, verbose) for c in cmds]:
                     f.result()
             _run([HIPCC, *ARCH, "-shared", "-fPIC", "-o", tmp_lib, *objs], verbose)
-    os.replace(tmp_lib, LIB)
-    return LIB
+    os.replace(tmp_lib, target)
+    return target
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--out", default=None, help="dev variant output path")
+    ap.add_argument("-D", dest="defs", action="append", default=[], help="extra -D definitions")
+    ap.add_argument("--src", default=None, help="dev variant source (must sit in csrc/ for its includes)")
+    a = ap.parse_args()
+    build(force=a.force, out=a.out, extra=[f"-D{d}" for d in a.defs], src=a.src)

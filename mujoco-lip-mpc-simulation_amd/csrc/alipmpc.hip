@@ -815,6 +815,52 @@ __device__ __forceinline__ bool chol_rows(R (&a)[n], R& myidg, int lane)
 }
 
 // ------------------------------------------------------------------------------------------------
+// Gauss-Jordan solve of the (regularised) KKT system in LDS: M = [K | rhs] (n x (n+1), row stride LD), one
+// wave, element e = lane + 64 q owns M[e / (n+1)][e % (n+1)].  Step p: pivot d = M[p][p] (an LDS broadcast;
+// for a symmetric matrix the pivots are the D of K = L D L^T, so "all pivots > 0" is exactly the Cholesky
+// positive-definiteness test the inertia correction needs), row p /= d, every other row -= M[i][p] row p.
+// All reads of a step precede its writes in program order and a wave's DS operations execute in order, so
+// no barrier is needed.  n steps of ~3 LDS reads + 1 write per element group replace the register
+// Cholesky's O(n^2) readlane broadcasts and the two sequential triangular sweeps.  On success column n
+// holds the solution.
+// ------------------------------------------------------------------------------------------------
+template <int n, int LD, class R>
+__device__ __forceinline__ bool gj_lds(R* M, int lane)
+{
+    constexpr int NE = n * (n + 1), Q = (NE + WAVE - 1) / WAVE;
+    // lanes past the last element work on the padding element M[n][n] (row n is not part of the system),
+    // so every step is branch-free: elements with j <= p are rewritten unchanged
+    int ei[Q], ej[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        const int e = lane + WAVE * q;
+        ei[q] = e < NE ? e / (n + 1) : n;
+        ej[q] = e < NE ? e - (e / (n + 1)) * (n + 1) : n;
+    }
+#pragma unroll
+    for (int p = 0; p < n; ++p) {
+        const R d = M[p * LD + p];
+        if (!(d > R(0))) return false;   // wave-uniform: every lane read the same pivot
+        const R inv = rcp_nr(d);
+        R mip[Q], mpj[Q], mij[Q];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            mip[q] = M[ei[q] * LD + p];
+            mpj[q] = M[p * LD + ej[q]];
+            mij[q] = M[ei[q] * LD + ej[q]];
+        }
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const R f = mpj[q] * inv;
+            const R upd = ei[q] == p ? f : fma(-mip[q], f, mij[q]);
+            M[ei[q] * LD + ej[q]] = ej[q] > p ? upd : mij[q];
+        }
+        wave_sync();
+    }
+    return true;
+}
+
+// ------------------------------------------------------------------------------------------------
 // solve-kernel workspace.  Rows r < mr4 are the padded constraint rows; rows mr4 .. mr4+N-1 are the
 // objective terms f_k (k = 1..N) treated as pseudo-rows ("OBJ rows"): same generator-form gradient, so
 // grad f and J^T y come out of ONE J-layout sweep, and grad f . dV out of the row-layout dS pass.
@@ -1259,6 +1305,17 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
 
     STAMP_DECL
     for (it = 0; it <= max_iter; ++it) {
+        // A batch finishes with its slowest instance, and the 4 waves sharing a SIMD compete for issue: waves
+        // that have run long get priority, so the critical (high-iteration) instances run closer to their
+        // lone-wave latency while the short ones, which have slack, yield.
+#ifndef ALIP_NO_SETPRIO
+        if (it == 8)
+            __builtin_amdgcn_s_setprio(1);
+        else if (it == 14)
+            __builtin_amdgcn_s_setprio(2);
+        else if (it == 20)
+            __builtin_amdgcn_s_setprio(3);
+#endif
         R gl[NT];                                  // J^T y - grad f  (per column, all lanes)
         R jv[JC ? KSM : 1][NT];
         for (;;) {
@@ -1326,13 +1383,13 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
                 if (HL(q)) comp0 = fmax(comp0, fabs(dl * zl[q]));
                 if (HU(q)) comp0 = fmax(comp0, fabs(du * zu[q]));
             }
-            ru = wmax(ru);
-            rcm = wmax(rcm);
+            // (max(ru)/sd == max(ru/sd): division by sd > 0 and its rounding are monotone, so the stationarity
+            // and feasibility maxima share one reduction)
             nz = wsum(nz);
-            comp0 = wmax(comp0);
             const R sd = uni(fmax(R(100.0), nz / (w.cst[K_MACT] + n)) / R(100.0));
             const R sc = uni(fmax(R(100.0), nz / fmax(R(1.0), w.cst[K_NBL])) / R(100.0));
-            const R base_err = uni(fmax(ru / sd, rcm));
+            const R base_err = wmax(fmax(ru / sd, rcm));
+            comp0 = wmax(comp0);
             e0 = uni(fmax(base_err, comp0 / sc));
             if (e0 <= w.cst[K_TOL]) {
                 status = 0;
@@ -1461,60 +1518,45 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
         }
         wave_sync();
         STAMP(4);
-        // ---- factor with inertia correction, solve for dp
+        // ---- factor with inertia correction, solve for dp: Gauss-Jordan on [K + dw I | rhs] in LDS (gj_lds)
         RELANE();
         R xv;
         {
             R rhs_l = R(0.0);
 #pragma unroll
             for (int T = 0; T < NT; ++T) rhs_l = (lane < n && (lane >> 4) == T) ? rhsc[T] : rhs_l;
+            // lane i keeps row i of K (restores the matrix for an inertia-correction retry)
             R a[n];
-            R myidg = R(1.0);
 #pragma unroll
-            for (int j = 0; j < n; ++j) a[j] = lane < n ? w.K[lane * KLD + j] : (lane == j ? R(1.0) : R(0.0));
-            if (!chol_rows<n>(a, myidg, lane)) {
+            for (int j = 0; j < n; ++j) a[j] = lane < n ? w.K[lane * KLD + j] : R(0.0);
+            if (lane < n) w.K[lane * KLD + n] = rhs_l;
+            wave_sync();
+            if (!gj_lds<n, KLD>(w.K, lane)) {
                 R dw = dw_last == R(0.0) ? R(1e-4) : fmax(R(1e-20), dw_last / R(3.0));
                 for (;;) {
+                    if (lane < n) {
 #pragma unroll
-                    for (int j = 0; j < n; ++j)
-                        a[j] = (lane < n ? w.K[lane * KLD + j] : (lane == j ? R(1.0) : R(0.0))) + (lane == j ? dw : R(0.0));
-                    if (chol_rows<n>(a, myidg, lane)) break;
+                        for (int j = 0; j < n; ++j) w.K[lane * KLD + j] = a[j] + (lane == j ? dw : R(0.0));
+                        w.K[lane * KLD + n] = rhs_l;
+                    }
+                    wave_sync();
+                    if (gj_lds<n, KLD>(w.K, lane)) break;
                     dw *= dw_last == R(0.0) ? R(100.0) : R(8.0);
                     if (dw > R(sizeof(R) == 8 ? 1e40 : 1e30)) break;
                 }
                 dw_last = uni(dw);
             }
-            // forward: L y = rhs
-            R acc = R(0.0), yv = R(0.0);
-#pragma unroll
-            for (int k = 0; k < n; ++k) {
-                const R yk = bcast((rhs_l - acc) * myidg, k);
-                yv = lane == k ? yk : yv;
-                acc += lane > k ? a[k] * yk : R(0.0);
-            }
-            // transpose L through LDS for the backward sweep
-            wave_sync();
-            if (lane < n) {
-#pragma unroll
-                for (int j = 0; j < n; ++j) w.K[lane * KLD + j] = j <= lane ? a[j] : R(0.0);
-            }
-            wave_sync();
-            acc = R(0.0);
-            xv = R(0.0);
-#pragma unroll
-            for (int i = n - 1; i >= 0; --i) {
-                const R xi = bcast((yv - acc) * myidg, i);
-                xv = lane == i ? xi : xv;
-                acc += lane < i ? w.K[i * KLD + (lane & 31)] * xi : R(0.0);
-            }
+            xv = lane < n ? w.K[lane * KLD + n] : R(0.0);
         }
         STAMP(5);
-        // ---- dV = G dp (lane t), rows pick up their 4 entries
+        // ---- dV = G dp (lane t), rows pick up their 4 entries; dp is column n of the eliminated system in
+        // LDS (broadcast reads)
         RELANE();
+        (void)xv;
         {
             R v = R(0.0);
 #pragma unroll
-            for (int j = 0; j < n; ++j) v += G[(lane < NG ? lane : 0) * NCP + j] * bcast(xv, j);
+            for (int j = 0; j < n; ++j) v += G[(lane < NG ? lane : 0) * NCP + j] * w.K[j * KLD + n];
             dvme = lane < NG ? v : R(0.0);
             if (lane < NG) w.dV[lane] = dvme;
         }
