@@ -837,7 +837,7 @@ __device__ __forceinline__ bool gj_lds(R* M, int lane)
         ei[q] = e < NE ? e / (n + 1) : n;
         ej[q] = e < NE ? e - (e / (n + 1)) * (n + 1) : n;
     }
-#pragma unroll
+#pragma unroll 1
     for (int p = 0; p < n; ++p) {
         const R d = M[p * LD + p];
         if (!(d > R(0))) return false;   // wave-uniform: every lane read the same pivot
@@ -858,6 +858,32 @@ __device__ __forceinline__ bool gj_lds(R* M, int lane)
         wave_sync();
     }
     return true;
+}
+
+// working copy for gj_lds: M[i][j] = K[i][j] + dw [i == j] (j <= n; column n = rhs), same element
+// ownership as gj_lds (the padding element M[n][n] = 0)
+template <int n, int LDK, int LD, class R>
+__device__ __forceinline__ void gj_fill(const R* K, R* M, int lane, R dw)
+{
+    constexpr int NE = n * (n + 1), Q = (NE + WAVE - 1) / WAVE;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        const int e = lane + WAVE * q;
+        const int i = e < NE ? e / (n + 1) : n, j = e < NE ? e - (e / (n + 1)) * (n + 1) : n;
+        const R v = e < NE ? K[i * LDK + j] : R(0);
+        M[i * LD + j] = v + (i == j && e < NE ? dw : R(0));
+    }
+}
+template <int n, int LD, class R>
+__device__ __forceinline__ void gj_zero(R* M, int lane)
+{
+    constexpr int NE = n * (n + 1), Q = (NE + WAVE - 1) / WAVE;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        const int e = lane + WAVE * q;
+        const int i = e < NE ? e / (n + 1) : n, j = e < NE ? e - (e / (n + 1)) * (n + 1) : n;
+        M[i * LD + j] = R(0);
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1147,6 +1173,9 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
     constexpr int KLD = D::KLD;
     constexpr int RPL = (4 * KSM + WAVE - 1) / WAVE;
     constexpr bool JC = KSM * NT <= 16;   // keep the J tile in registers between the two J-layout passes
+    constexpr bool GJ = n <= 9;           // KKT solve: LDS Gauss-Jordan (small n) or register Cholesky
+    constexpr int GJLD = n + 1;           // row stride of the Gauss-Jordan working copy (in the S buffer)
+    static_assert((n + 1) * (n + 1) <= 64 * (N + 1), "GJ working copy fits the S-block buffer");
     static_assert(NG <= WAVE, "one generator row per lane");
     extern __shared__ __attribute__((aligned(16))) double smem[];
     KP* Ps = reinterpret_cast<KP*>(smem);
@@ -1518,49 +1547,91 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
         }
         wave_sync();
         STAMP(4);
-        // ---- factor with inertia correction, solve for dp: Gauss-Jordan on [K + dw I | rhs] in LDS (gj_lds)
+        // ---- factor with inertia correction, solve for dp.  n <= 9 (N <= 3): Gauss-Jordan on [K + dw I | rhs]
+        // in LDS (gj_lds); larger n: register Cholesky (chol_rows) + two triangular sweeps, which measured
+        // faster there (GJ work grows as n * ceil(n (n+1) / 64) element updates)
         RELANE();
         R xv;
         {
             R rhs_l = R(0.0);
 #pragma unroll
             for (int T = 0; T < NT; ++T) rhs_l = (lane < n && (lane >> 4) == T) ? rhsc[T] : rhs_l;
-            // lane i keeps row i of K (restores the matrix for an inertia-correction retry)
-            R a[n];
-#pragma unroll
-            for (int j = 0; j < n; ++j) a[j] = lane < n ? w.K[lane * KLD + j] : R(0.0);
-            if (lane < n) w.K[lane * KLD + n] = rhs_l;
-            wave_sync();
-            if (!gj_lds<n, KLD>(w.K, lane)) {
-                R dw = dw_last == R(0.0) ? R(1e-4) : fmax(R(1e-20), dw_last / R(3.0));
-                for (;;) {
-                    if (lane < n) {
-#pragma unroll
-                        for (int j = 0; j < n; ++j) w.K[lane * KLD + j] = a[j] + (lane == j ? dw : R(0.0));
-                        w.K[lane * KLD + n] = rhs_l;
+            if constexpr (GJ) {
+                // [K | rhs] stays in w.K (the original, for inertia-correction retries); the elimination runs on
+                // a copy in the S-block buffer, which is dead once K is built and is re-zeroed after dV below
+                if (lane < n) w.K[lane * KLD + n] = rhs_l;
+                wave_sync();
+                gj_fill<n, KLD, GJLD>(w.K, w.S, lane, R(0));
+                wave_sync();
+                if (!gj_lds<n, GJLD>(w.S, lane)) {
+                    R dw = dw_last == R(0.0) ? R(1e-4) : fmax(R(1e-20), dw_last / R(3.0));
+                    for (;;) {
+                        gj_fill<n, KLD, GJLD>(w.K, w.S, lane, dw);
+                        wave_sync();
+                        if (gj_lds<n, GJLD>(w.S, lane)) break;
+                        dw *= dw_last == R(0.0) ? R(100.0) : R(8.0);
+                        if (dw > R(sizeof(R) == 8 ? 1e40 : 1e30)) break;
                     }
-                    wave_sync();
-                    if (gj_lds<n, KLD>(w.K, lane)) break;
-                    dw *= dw_last == R(0.0) ? R(100.0) : R(8.0);
-                    if (dw > R(sizeof(R) == 8 ? 1e40 : 1e30)) break;
+                    dw_last = uni(dw);
                 }
-                dw_last = uni(dw);
+                xv = lane < n ? w.S[lane * GJLD + n] : R(0.0);
+            } else {
+                R a[n];
+                R myidg = R(1.0);
+#pragma unroll
+                for (int j = 0; j < n; ++j) a[j] = lane < n ? w.K[lane * KLD + j] : (lane == j ? R(1.0) : R(0.0));
+                if (!chol_rows<n>(a, myidg, lane)) {
+                    R dw = dw_last == R(0.0) ? R(1e-4) : fmax(R(1e-20), dw_last / R(3.0));
+                    for (;;) {
+#pragma unroll
+                        for (int j = 0; j < n; ++j)
+                            a[j] = (lane < n ? w.K[lane * KLD + j] : (lane == j ? R(1.0) : R(0.0))) +
+                                   (lane == j ? dw : R(0.0));
+                        if (chol_rows<n>(a, myidg, lane)) break;
+                        dw *= dw_last == R(0.0) ? R(100.0) : R(8.0);
+                        if (dw > R(sizeof(R) == 8 ? 1e40 : 1e30)) break;
+                    }
+                    dw_last = uni(dw);
+                }
+                // forward: L y = rhs
+                R acc = R(0.0), yv = R(0.0);
+#pragma unroll
+                for (int k = 0; k < n; ++k) {
+                    const R yk = bcast((rhs_l - acc) * myidg, k);
+                    yv = lane == k ? yk : yv;
+                    acc += lane > k ? a[k] * yk : R(0.0);
+                }
+                // transpose L through LDS for the backward sweep
+                wave_sync();
+                if (lane < n) {
+#pragma unroll
+                    for (int j = 0; j < n; ++j) w.K[lane * KLD + j] = j <= lane ? a[j] : R(0.0);
+                }
+                wave_sync();
+                acc = R(0.0);
+                xv = R(0.0);
+#pragma unroll
+                for (int i = n - 1; i >= 0; --i) {
+                    const R xi = bcast((yv - acc) * myidg, i);
+                    xv = lane == i ? xi : xv;
+                    acc += lane < i ? w.K[i * KLD + (lane & 31)] * xi : R(0.0);
+                }
             }
-            xv = lane < n ? w.K[lane * KLD + n] : R(0.0);
         }
         STAMP(5);
-        // ---- dV = G dp (lane t), rows pick up their 4 entries; dp is column n of the eliminated system in
-        // LDS (broadcast reads)
+        // ---- dV = G dp (lane t), rows pick up their 4 entries; GJ: dp is column n of the eliminated system
+        // in LDS (broadcast reads), Cholesky: dp is in lane registers (readlane)
         RELANE();
-        (void)xv;
         {
             R v = R(0.0);
 #pragma unroll
-            for (int j = 0; j < n; ++j) v += G[(lane < NG ? lane : 0) * NCP + j] * w.K[j * KLD + n];
+            for (int j = 0; j < n; ++j)
+                v += G[(lane < NG ? lane : 0) * NCP + j] * (GJ ? w.S[j * GJLD + n] : bcast(xv, j));
             dvme = lane < NG ? v : R(0.0);
             if (lane < NG) w.dV[lane] = dvme;
         }
         wave_sync();
+        if constexpr (GJ) gj_zero<n, GJLD>(w.S, lane);   // hess_blocks writes only the nonzero pattern of S
         // ---- slack / multiplier steps, fraction to boundary
         RELANE();
         R dS[RPL], dZl[RPL], dZu[RPL];
