@@ -10,6 +10,7 @@ Default workload = BASELINE configs[1] ("cfg2"): B = 4096 random ALIP initial st
 own shard (scenes are generated from (seed, rank)) and each step ends with one RCCL gather of the
 per-instance outputs to rank 0 — the path has no other exchange.
 The other BASELINE configs are presets (not the driver's default line):
+  cfg1  B = 1, N = 3, no obstacles, sig_step (the reference's own CPU-runnable case: single-solve latency)
   cfg3  B = 65,536 per GPU, N = 5, 5 circles + 5 ellipses, fp64 (weak scaling)
   cfg4  262,144 instances in total sharded over the GPUs, N = 3, 5 circles, fp64 (strong scaling)
   cfg5  1,048,576 randomized scenes in total (one obstacle field each), N = 3, fp32 solve kernels;
@@ -36,6 +37,7 @@ FP32_PEAK_TFLOPS = 157.3     # MI355X FP32 matrix = vector peak (MI355X_MICROARC
 
 # BASELINE.json configs: (instances, per_gpu?, horizon, circles, ellipses, precision, distinct fields)
 CONFIGS = {
+    "cfg1": dict(batch=1, per_gpu=True, horizon=3, circles=0, ellipses=0, fp32=False, variant="sig_step"),
     "cfg2": dict(batch=4096, per_gpu=True, horizon=3, circles=5, ellipses=0, fp32=False),
     "cfg3": dict(batch=65536, per_gpu=True, horizon=5, circles=5, ellipses=5, fp32=False),
     "cfg4": dict(batch=262144, per_gpu=False, horizon=3, circles=5, ellipses=0, fp32=False),
@@ -67,7 +69,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=None, help="instances per GPU (default: the config's)")
-    ap.add_argument("--variant", default="modi", choices=["modi", "sig_step"])
+    ap.add_argument("--variant", default=None, choices=["modi", "sig_step"], help="default: the config's (modi)")
     ap.add_argument("--horizon", type=int, default=None)
     ap.add_argument("--obstacles", type=int, default=None, help="circles per instance")
     ap.add_argument("--seed", type=int, default=0)
@@ -96,8 +98,9 @@ def main():
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a visible MI355X (torch.cuda.is_available() is False)")
 
-    variant = {"modi": alipmpc.VARIANT_MODI, "sig_step": alipmpc.VARIANT_SIG_STEP}[args.variant]
     preset = CONFIGS[args.config]
+    args.variant = args.variant or preset.get("variant", "modi")
+    variant = {"modi": alipmpc.VARIANT_MODI, "sig_step": alipmpc.VARIANT_SIG_STEP}[args.variant]
     N = args.horizon or preset["horizon"]
     n_cir = preset["circles"] if args.obstacles is None else args.obstacles
     n_elp = preset["ellipses"]

@@ -2,7 +2,7 @@
 import os, sys, ctypes
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["ALIPMPC_LIB"] = os.path.join(ROOT, "mujoco-lip-mpc-simulation_amd", "alipmpc", sys.argv[1] if len(sys.argv) > 1 else "libalipmpc_stamps.so")
+os.environ["ALIPMPC_LIB"] = os.path.join(ROOT, sys.argv[1] if len(sys.argv) > 1 else "devlib/libalipmpc_stamps.so")
 sys.path.insert(0, os.path.join(ROOT, "mujoco-lip-mpc-simulation_amd"))
 import alipmpc
 from alipmpc import scenes
