@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Benchmark: batched ALIP-MPC-CBF solves/sec on MI355X (BASELINE.json metric).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4|cfg5] [--batch B] ...
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg1|cfg2|cfg3|cfg4|cfg5] [--batch B] ...
 
 One "step" = one fused interior-point solve of a batch of B independent NLP instances whose inputs are
 already resident in HBM (one launch of solve_kernel through the C ABI on the current HIP stream).
