@@ -1890,9 +1890,10 @@ __global__ __launch_bounds__(256, 4) void eval_kernel(KP Pv)
     const KP& P = *Ps;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);   // wave-uniform (SGPR)
     const int lane = lane_id();
-    const long long b = (long long)blockIdx.x * WAVES_PER_BLOCK + wv;
-    if (b >= P.B) return;
     WS<N> w = carve<N>(wsb + (size_t)wv * ws_doubles<N>(P.nc_max, P.ne_max, P.mr4), P.nc_max, P.ne_max, P.mr4);
+    // grid-stride over instances: the G/E staging above is paid once per workgroup, not per instance
+    for (long long b = (long long)blockIdx.x * WAVES_PER_BLOCK + wv; b < P.B;
+         b += (long long)gridDim.x * WAVES_PER_BLOCK) {
     double gxg, gyg, uj;
     int legv;
     prologue<N, true>(P, w, G, E, b, gxg, gyg, legv, uj);
@@ -1958,7 +1959,10 @@ __global__ __launch_bounds__(256, 4) void eval_kernel(KP Pv)
             P.goal_eff_out[2 * b + 1] = gyg;
         }
     }
+    wave_sync();
+    }
 }
+
 
 // ================================================================================================
 // DD variant: unicycle MPC-CBF (MPC_DD_sig_step.py:123-193 set-up, 320-572 LIP_Prob)
@@ -3099,8 +3103,10 @@ hipError_t launch_t(bool solve, bool f32, const KP& P, size_t smem, hipStream_t 
     } else if (solve) {
         launch_solve<N, double>(P, smem, st);
     } else {
+        // grid-stride eval kernel: at most 8 workgroups per CU resident at once on the 256 CUs
+        const unsigned egrid = grid < 2048u ? grid : 2048u;
         set_smem((const void*)eval_kernel<N>, smem);
-        hipLaunchKernelGGL(eval_kernel<N>, dim3(grid), dim3(WAVE * WAVES_PER_BLOCK), smem, st, P);
+        hipLaunchKernelGGL(eval_kernel<N>, dim3(egrid), dim3(WAVE * WAVES_PER_BLOCK), smem, st, P);
     }
     return hipGetLastError();
 }
