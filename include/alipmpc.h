@@ -62,6 +62,7 @@ extern "C" {
 #define ALIPMPC_SOLVED_TO_ACCEPTABLE_LEVEL 1
 #define ALIPMPC_INFEASIBLE_PROBLEM_DETECTED 2
 #define ALIPMPC_MAXIMUM_ITERATIONS_EXCEEDED (-1)
+#define ALIPMPC_ERROR_IN_STEP_COMPUTATION (-3)   /* KKT regularisation exhausted; last iterate returned */
 /* rollout only: the instance had already reached its goal, no solve was run at this step */
 #define ALIPMPC_ROLLOUT_DONE (-10)
 

@@ -16,7 +16,8 @@ VARIANT_MODI, VARIANT_SIG_STEP, VARIANT_DD = 0, 1, 2
 PREC_FP64, PREC_FP32 = 0, 1
 
 STATUS_NAMES = {0: "Solve_Succeeded", 1: "Solved_To_Acceptable_Level", 2: "Infeasible_Problem_Detected",
-                -1: "Maximum_Iterations_Exceeded", -10: "Rollout_Done (goal reached earlier, not solved)"}
+                -1: "Maximum_Iterations_Exceeded", -3: "Error_In_Step_Computation",
+                -10: "Rollout_Done (goal reached earlier, not solved)"}
 ROLLOUT_DONE = -10
 
 _ERRORS = {-1: "EINVAL", -2: "ENODEV (no visible gfx950 device)", -3: "EHIP", -4: "EUNSUPPORTED"}

@@ -1552,6 +1552,7 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
         // faster there (GJ work grows as n * ceil(n (n+1) / 64) element updates)
         RELANE();
         R xv;
+        bool fact_ok = true;   // false: regularisation exhausted (IPOPT's Error_In_Step_Computation)
         {
             R rhs_l = R(0.0);
 #pragma unroll
@@ -1570,7 +1571,10 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
                         wave_sync();
                         if (gj_lds<n, GJLD>(w.S, lane)) break;
                         dw *= dw_last == R(0.0) ? R(100.0) : R(8.0);
-                        if (dw > R(sizeof(R) == 8 ? 1e40 : 1e30)) break;
+                        if (dw > R(sizeof(R) == 8 ? 1e40 : 1e30)) {
+                            fact_ok = false;
+                            break;
+                        }
                     }
                     dw_last = uni(dw);
                 }
@@ -1589,7 +1593,10 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
                                    (lane == j ? dw : R(0.0));
                         if (chol_rows<n>(a, myidg, lane)) break;
                         dw *= dw_last == R(0.0) ? R(100.0) : R(8.0);
-                        if (dw > R(sizeof(R) == 8 ? 1e40 : 1e30)) break;
+                        if (dw > R(sizeof(R) == 8 ? 1e40 : 1e30)) {
+                            fact_ok = false;
+                            break;
+                        }
                     }
                     dw_last = uni(dw);
                 }
@@ -1632,6 +1639,10 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
         }
         wave_sync();
         if constexpr (GJ) gj_zero<n, GJLD>(w.S, lane);   // hess_blocks writes only the nonzero pattern of S
+        if (!fact_ok) {   // keep the last iterate (dV is scratch; V untouched)
+            status = -3;
+            break;
+        }
         // ---- slack / multiplier steps, fraction to boundary
         RELANE();
         R dS[RPL], dZl[RPL], dZu[RPL];
@@ -1831,7 +1842,7 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
     // ---- status + outputs (violation measured on the reference's exact |.|)
     wave_sync();
     RELANE();
-    if (status != 0 && status != 2) {
+    if (status != 0 && status != 2 && status != -3) {
         R viol = R(0.0);
 #pragma unroll
         for (int q = 0; q < RPL; ++q) {
@@ -2555,6 +2566,7 @@ __global__ __launch_bounds__(256, 4) void dd_solve_kernel(KP Pv)
         // ---- factor with inertia correction, solve for du
         RELANE();
         double xv;
+        bool fact_ok = true;
         {
             const double rhs_l = lane < n ? rhs : 0.0;
             double a[n];
@@ -2569,7 +2581,10 @@ __global__ __launch_bounds__(256, 4) void dd_solve_kernel(KP Pv)
                         a[j] = (lane < n ? w.K[lane * KLD + j] : (lane == j ? 1.0 : 0.0)) + (lane == j ? dw : 0.0);
                     if (chol_rows<n>(a, myidg, lane)) break;
                     dw *= dw_last == 0.0 ? 100.0 : 8.0;
-                    if (dw > 1e40) break;
+                    if (dw > 1e40) {
+                        fact_ok = false;
+                        break;
+                    }
                 }
                 dw_last = uni(dw);
             }
@@ -2597,6 +2612,10 @@ __global__ __launch_bounds__(256, 4) void dd_solve_kernel(KP Pv)
         }
         if (lane < 16) w.dU[lane] = lane < n ? xv : 0.0;
         wave_sync();
+        if (!fact_ok) {
+            status = -3;
+            break;
+        }
         // ---- slack / multiplier steps, fraction to boundary
         RELANE();
         double dS[RPL], dZl[RPL], dZu[RPL];
@@ -2784,7 +2803,7 @@ __global__ __launch_bounds__(256, 4) void dd_solve_kernel(KP Pv)
     // ---- status + outputs (split rows measure the reference's f_en violation exactly)
     wave_sync();
     RELANE();
-    if (status != 0 && status != 2) {
+    if (status != 0 && status != 2 && status != -3) {
         double viol = 0.0;
 #pragma unroll
         for (int q = 0; q < RPL; ++q) {

@@ -1100,6 +1100,7 @@ static void osolve(oprob* P, const double* u0, double* uout, osolve_info* info)
         }
         double L[OMAXV * OMAXV];
         double dw = 0.0;
+        int fact_ok = 1;
         memcpy(L, Kmat, sizeof(double) * n * n);
         if (!chol(L, n)) {
             dw = dw_last == 0 ? 1e-4 : fmax(1e-20, dw_last / 3.0);
@@ -1108,9 +1109,16 @@ static void osolve(oprob* P, const double* u0, double* uout, osolve_info* info)
                 for (int a = 0; a < n; ++a) L[a * n + a] += dw;
                 if (chol(L, n)) break;
                 dw *= dw_last == 0 ? 100.0 : 8.0;
-                if (dw > 1e40) break;
+                if (dw > 1e40) {
+                    fact_ok = 0;
+                    break;
+                }
             }
             dw_last = dw;
+        }
+        if (!fact_ok) {   /* regularisation exhausted: IPOPT's Error_In_Step_Computation, last iterate kept */
+            status = -3;
+            break;
         }
         memcpy(dU, rhs, sizeof(double) * n);
         cholsolve(L, n, dU);
@@ -1220,7 +1228,7 @@ static void osolve(oprob* P, const double* u0, double* uout, osolve_info* info)
 #undef ERR
     }
     free(ft);
-    if (status != 0 && status != 2) {
+    if (status != 0 && status != 2 && status != -3) {
         pcons(P, u, c);
         double viol = 0;
         for (int i = 0; i < m; ++i) {
