@@ -53,13 +53,14 @@ def flops_per_iter(n, m, N, nobs):
     return kkt + chol + nlp
 
 
-def solve_kernel_name(N, rps, modi, fp32=False):
-    """The solve_kernel<N, KSM> instance the library dispatches (csrc/alipmpc.hip: ksm_of): constraint rows
-    in the solve layout (f_en split into two rows for modi) + N objective rows, in 4-row J-layout steps."""
+def solve_kernel_name(N, rps, modi, fp32=False, queue=False):
+    """The solve_kernel<N, KSM, R, QUEUE> instance the library dispatches (csrc/alipmpc.hip: ksm_of,
+    launch_solve): constraint rows in the solve layout (f_en split into two rows for modi) + N objective
+    rows, in 4-row J-layout steps; QUEUE = the batch exceeds the resident instance slots."""
     m = N * (rps + (1 if modi else 0))
     rows = ((m + 3) // 4) * 4 + 4 * ((N + 3) // 4)
     ksm = next(k for k in (8, 10, 12, 16, 24, 32, 48) if rows <= 4 * k)
-    return f"solve_kernel<{N},{ksm},{'float' if fp32 else 'double'}>", m
+    return f"solve_kernel<{N},{ksm},{'float' if fp32 else 'double'},{'true' if queue else 'false'}>", m
 
 
 def parse():
@@ -192,7 +193,12 @@ def main():
     total_solves = B_total * K
     value = total_solves / elapsed
     # roofline of the dominant kernel (solve_kernel): algorithmic FP64 flops per launch / launch time
-    kname, m = solve_kernel_name(N, solver.rps, variant == alipmpc.VARIANT_MODI, fp32)
+    try:
+        slots = solver.solve_slots()
+    except (AttributeError, RuntimeError):
+        slots = None
+    kname, m = solve_kernel_name(N, solver.rps, variant == alipmpc.VARIANT_MODI, fp32,
+                                 queue=slots is not None and B > slots)
     fpi = flops_per_iter(n, m, N, n_cir + n_elp)
     peak = FP32_PEAK_TFLOPS if fp32 else FP64_PEAK_TFLOPS
     launch_flops = fpi * float(iters.sum())
@@ -241,6 +247,8 @@ def main():
                 "variant": args.variant, "parallelism": f"shard{world}" if world > 1 else "single",
                 "mean_iters": float(iters.mean()), "max_iters": int(iters.max()),
                 "status_counts": {str(k): int(v) for k, v in zip(*np.unique(status, return_counts=True))},
+                "resident_slots": slots,
+                "launch": "persistent work queue" if (slots is not None and B > slots) else "one wave per instance",
             },
             "roofline": {
                 "kernel": kname,

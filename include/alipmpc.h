@@ -196,6 +196,14 @@ int32_t alipmpc_trace_len(const alipmpc_cfg* cfg);
 int alipmpc_trace_batch(void* handle, int64_t B, const double* x0, const double* u, double* trace,
                         void* hip_stream);
 
+/* Instances this handle's solve kernel holds resident on its device at once (resident workgroups x 4
+ * waves, one instance per wave).  A solve_batch / rollout with more instances than this runs a persistent
+ * grid of exactly the resident workgroups that pulls instances from a per-launch work queue (a wave that
+ * finishes a short solve takes the next instance); smaller batches launch one wave per instance.  The
+ * per-instance results do not depend on the launch form.  0 for the DD variant (always one wave per
+ * instance).  No reference counterpart (scheduling of the batched replacement). */
+int alipmpc_solve_slots(void* handle, int64_t* slots);
+
 /* Duration in milliseconds of the most recent solve kernel launch on this handle, measured with HIP
  * events on the launch stream (0 if none). */
 double alipmpc_last_kernel_ms(void* handle);

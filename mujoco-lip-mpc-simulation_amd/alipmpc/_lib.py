@@ -37,7 +37,8 @@ class Cfg(ctypes.Structure):
 
 EXPORTS = ("alipmpc_default_cfg", "alipmpc_rows_per_step", "alipmpc_num_vars", "alipmpc_create",
            "alipmpc_solve_batch", "alipmpc_eval_batch", "alipmpc_rollout_batch", "alipmpc_trace_len",
-           "alipmpc_trace_batch", "alipmpc_last_kernel_ms", "alipmpc_last_error", "alipmpc_destroy")
+           "alipmpc_trace_batch", "alipmpc_solve_slots", "alipmpc_last_kernel_ms", "alipmpc_last_error",
+           "alipmpc_destroy")
 
 _lib = None
 
@@ -78,6 +79,9 @@ def load(build_if_missing=True):
     L.alipmpc_trace_len.restype = ctypes.c_int32
     L.alipmpc_trace_batch.argtypes = [P, ctypes.c_int64, P, P, P, P]
     L.alipmpc_trace_batch.restype = ctypes.c_int
+    if hasattr(L, "alipmpc_solve_slots"):     # (absent from older dev builds used for A/B timing)
+        L.alipmpc_solve_slots.argtypes = [P, ctypes.POINTER(ctypes.c_int64)]
+        L.alipmpc_solve_slots.restype = ctypes.c_int
     L.alipmpc_last_kernel_ms.argtypes = [P]
     L.alipmpc_last_kernel_ms.restype = ctypes.c_double
     L.alipmpc_last_error.argtypes = [P]
@@ -179,6 +183,13 @@ class Solver:
 
     def last_kernel_ms(self):
         return float(self._L.alipmpc_last_kernel_ms(self._h))
+
+    def solve_slots(self):
+        """Instances the solve kernel holds resident at once; larger batches run the persistent
+        work-queue launch (include/alipmpc.h: alipmpc_solve_slots)."""
+        v = ctypes.c_int64(0)
+        self._check(self._L.alipmpc_solve_slots(self._h, ctypes.byref(v)), "alipmpc_solve_slots")
+        return int(v.value)
 
     # ---------------------------------------------------------------- host (numpy) calls
     def _inputs(self, x0, goal, leg, cir, nc, elp, ne):

@@ -29,6 +29,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -76,6 +77,7 @@ struct KP {
     const double* u0;
     const double* last_u;   // DD: previous control (B x 2)
     const uint8_t* active;  // nullable: instances with active[b] == 0 are skipped (closed-loop rollouts)
+    uint32_t* queue;        // nullable: work-queue counters of a persistent solve launch (solve_kernel)
     // solve outputs
     double* u_out;
     double* foot_out;
@@ -1162,9 +1164,13 @@ __device__ void hess_blocks(const WSS<N, R>& w, int lane, int rps, int nobs, int
 //   J layout (lane = (g4, col), rows 4s + g4, KSM steps, fully unrolled): J^T y, grad f, J^T w and the
 //   MFMA KKT products.
 // ------------------------------------------------------------------------------------------------
-template <int N, int KSM, class R>
-__global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
+template <int N, int KSM, class R, bool Q>
+__device__ __forceinline__ void solve_one(const KP& P, R* G, R* E, R* wsb, int wv, long long b)
 {
+    // Q (persistent instance loop): opaque per-instance copies of the lane-/wave-derived inputs, so that
+    // nothing computed from them is loop-invariant and no address or row table is hoisted out of the
+    // instance loop (and spilled)
+    if constexpr (Q) asm volatile("" : "+s"(wv), "+s"(b));
     using D = Dim<N>;
     constexpr int n = D::n;
     constexpr int NT = D::NT;
@@ -1177,21 +1183,11 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
     constexpr int GJLD = n + 1;           // row stride of the Gauss-Jordan working copy (in the S buffer)
     static_assert((n + 1) * (n + 1) <= 64 * (N + 1), "GJ working copy fits the S-block buffer");
     static_assert(NG <= WAVE, "one generator row per lane");
-    extern __shared__ __attribute__((aligned(16))) double smem[];
-    KP* Ps = reinterpret_cast<KP*>(smem);
-    R* G = reinterpret_cast<R*>(smem + KP_DOUBLES);
-    R* E = G + NG * NCP;
-    R* wsb = E + ((NG * 5 + 3) & ~3);
-    if (threadIdx.x == 0) *Ps = Pv;
-    for (int i = threadIdx.x; i < NG * NCP; i += blockDim.x) G[i] = Pv.G[i];
-    for (int i = threadIdx.x; i < NG * 5; i += blockDim.x) E[i] = Pv.E[i];
-    __syncthreads();
-    const KP& P = *Ps;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);   // wave-uniform (SGPR)
     int lane = lane_id();
-    const long long b = (long long)blockIdx.x * WAVES_PER_BLOCK + wv;
-    if (b >= P.B) return;
-    if (P.active && !P.active[b]) return;   // rollout: instance already at its goal
+    if constexpr (Q) RELAUNDER(lane);
+#ifndef ALIP_NO_SETPRIO
+    __builtin_amdgcn_s_setprio(0);   // a persistent wave starts each instance at base priority
+#endif
     // uniform problem sizes in SGPRs (P lives in LDS: a plain read would be a per-lane VGPR value)
     const int mr4 = rfl(P.mr4), mo4 = rfl(P.mo4), m_max = rfl(P.m_max), rps = rfl(P.rps);
     const int nc_max = rfl(P.nc_max), ne_max = rfl(P.ne_max), nobs = nc_max + ne_max;
@@ -1874,6 +1870,56 @@ __global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
 #undef CK
 #undef HL
 #undef HU
+}
+
+// work-queue instance source of a persistent launch: counters q[0] (next instance) and q[1] (waves that
+// found the queue empty); the last wave out resets both, so the next launch on the stream starts at 0
+__device__ __forceinline__ long long next_instance(uint32_t* q)
+{
+    uint32_t v = 0;
+    if (lane_id() == 0) v = atomicAdd(q, 1u);
+    return (long long)__builtin_amdgcn_readfirstlane(v);
+}
+
+__device__ __forceinline__ void queue_exit(uint32_t* q)
+{
+    __threadfence();
+    if (lane_id() == 0 && atomicAdd(q + 1, 1u) == gridDim.x * WAVES_PER_BLOCK - 1) {
+        atomicExch(q, 0u);
+        atomicExch(q + 1, 0u);
+    }
+}
+
+template <int N, int KSM, class R, bool QUEUE>
+__global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
+{
+    using D = Dim<N>;
+    constexpr int NCP = D::NCP;
+    constexpr int NG = D::NG;
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    KP* Ps = reinterpret_cast<KP*>(smem);
+    R* G = reinterpret_cast<R*>(smem + KP_DOUBLES);
+    R* E = G + NG * NCP;
+    R* wsb = E + ((NG * 5 + 3) & ~3);
+    if (threadIdx.x == 0) *Ps = Pv;
+    for (int i = threadIdx.x; i < NG * NCP; i += blockDim.x) G[i] = Pv.G[i];
+    for (int i = threadIdx.x; i < NG * 5; i += blockDim.x) E[i] = Pv.E[i];
+    __syncthreads();
+    const KP& P = *Ps;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);   // wave-uniform (SGPR)
+    // QUEUE = false: one instance per wave.  QUEUE = true (more instances than resident wave slots): a
+    // persistent grid of the resident workgroups pulls instances from the launch's work queue, so that a
+    // wave that finishes a short solve takes the next instance instead of idling until its workgroup's
+    // longest solve ends (a workgroup's slots are only refilled as a whole)
+    if constexpr (!QUEUE) {
+        const long long b = (long long)blockIdx.x * WAVES_PER_BLOCK + wv;
+        if (b < Pv.B && (!Pv.active || Pv.active[b])) solve_one<N, KSM, R, false>(P, G, E, wsb, wv, b);
+    } else {
+        uint32_t* const q = Pv.queue;
+        for (long long b = next_instance(q); b < Pv.B; b = next_instance(q))
+            if (!Pv.active || Pv.active[b]) solve_one<N, KSM, R, true>(P, G, E, wsb, wv, b);   // rollout: skip finished
+        queue_exit(q);
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -3085,42 +3131,76 @@ static void set_smem(const void* f, size_t smem)
     d[f] = smem;
 }
 
-template <int N, class R>
-void launch_solve(const KP& P, size_t smem, hipStream_t st)
+// workgroups of kernel f resident on the whole device at once (occupancy x CUs), cached per (f, smem)
+static unsigned resident_blocks(const void* f, size_t smem)
 {
-    const unsigned grid = (unsigned)((P.B + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
+    static std::mutex mtx;
+    static std::map<std::pair<const void*, size_t>, unsigned> cache[64];
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(mtx);
+    auto& c = cache[dev & 63];
+    auto it = c.find({f, smem});
+    if (it != c.end()) return it->second;
+    int per_cu = 0, cus = 0;
+    unsigned r = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, WAVE * WAVES_PER_BLOCK, smem) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && per_cu > 0 && cus > 0)
+        r = (unsigned)per_cu * (unsigned)cus;
+    c[{f, smem}] = r;
+    return r;
+}
+
+template <int N, class R>
+void launch_solve(const KP& P0, size_t smem, hipStream_t st, unsigned* res_out)
+{
+    const unsigned need = (unsigned)((P0.B + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
     {
         // KSM = 4-row steps of the J layout, the smallest compiled size covering mo4 rows
-        auto go = [&](auto kern) {
-            set_smem((const void*)kern, smem);
-            hipLaunchKernelGGL(kern, dim3(grid), dim3(WAVE * WAVES_PER_BLOCK), smem, st, P);
+        auto go = [&](auto kern, auto kern_q) {
+            // more instances than resident wave slots: a persistent grid of exactly the resident
+            // workgroups pulls instances from the work queue; otherwise one instance per wave
+            set_smem((const void*)kern_q, smem);
+            const unsigned res = resident_blocks((const void*)kern_q, smem);
+            if (res_out) {   // query only (alipmpc_solve_slots)
+                *res_out = res;
+                return;
+            }
+            if (P0.queue && res > 0 && need > res && P0.B < (1LL << 31)) {
+                hipLaunchKernelGGL(kern_q, dim3(res), dim3(WAVE * WAVES_PER_BLOCK), smem, st, P0);
+            } else {
+                KP P = P0;
+                P.queue = nullptr;
+                set_smem((const void*)kern, smem);
+                hipLaunchKernelGGL(kern, dim3(need), dim3(WAVE * WAVES_PER_BLOCK), smem, st, P);
+            }
         };
-        if (P.mo4 <= 32)
-            go(solve_kernel<N, 8, R>);
-        else if (P.mo4 <= 40)
-            go(solve_kernel<N, 10, R>);
-        else if (P.mo4 <= 48)
-            go(solve_kernel<N, 12, R>);
-        else if (P.mo4 <= 64)
-            go(solve_kernel<N, 16, R>);
-        else if (P.mo4 <= 96)
-            go(solve_kernel<N, 24, R>);
-        else if (P.mo4 <= 128)
-            go(solve_kernel<N, 32, R>);
+        if (P0.mo4 <= 32)
+            go(solve_kernel<N, 8, R, false>, solve_kernel<N, 8, R, true>);
+        else if (P0.mo4 <= 40)
+            go(solve_kernel<N, 10, R, false>, solve_kernel<N, 10, R, true>);
+        else if (P0.mo4 <= 48)
+            go(solve_kernel<N, 12, R, false>, solve_kernel<N, 12, R, true>);
+        else if (P0.mo4 <= 64)
+            go(solve_kernel<N, 16, R, false>, solve_kernel<N, 16, R, true>);
+        else if (P0.mo4 <= 96)
+            go(solve_kernel<N, 24, R, false>, solve_kernel<N, 24, R, true>);
+        else if (P0.mo4 <= 128)
+            go(solve_kernel<N, 32, R, false>, solve_kernel<N, 32, R, true>);
         else
-            go(solve_kernel<N, 48, R>);
+            go(solve_kernel<N, 48, R, false>, solve_kernel<N, 48, R, true>);
     }
 }
 
 // solve kernels run in the handle's precision (cfg.precision); the eval hook is always fp64
 template <int N>
-hipError_t launch_t(bool solve, bool f32, const KP& P, size_t smem, hipStream_t st)
+hipError_t launch_t(bool solve, bool f32, const KP& P, size_t smem, hipStream_t st, unsigned* res_out)
 {
     const unsigned grid = (unsigned)((P.B + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
     if (solve && f32) {
-        launch_solve<N, float>(P, smem, st);
+        launch_solve<N, float>(P, smem, st, res_out);
     } else if (solve) {
-        launch_solve<N, double>(P, smem, st);
+        launch_solve<N, double>(P, smem, st, res_out);
     } else {
         // grid-stride eval kernel: at most 8 workgroups per CU resident at once on the 256 CUs
         const unsigned egrid = grid < 2048u ? grid : 2048u;
@@ -3150,16 +3230,18 @@ hipError_t launch_dd(bool solve, const KP& P, size_t smem, hipStream_t st)
 }
 
 #define ALIP_LAUNCHERS(k)                                                                              \
-    hipError_t launch_lip_##k(bool solve, bool f32, const KP& P, size_t smem, hipStream_t st)          \
+    hipError_t launch_lip_##k(bool solve, bool f32, const KP& P, size_t smem, hipStream_t st,          \
+                              unsigned* res_out)                                                       \
     {                                                                                                  \
-        return launch_t<k>(solve, f32, P, smem, st);                                                   \
+        return launch_t<k>(solve, f32, P, smem, st, res_out);                                          \
     }                                                                                                  \
     hipError_t launch_dd_##k(bool solve, const KP& P, size_t smem, hipStream_t st)                     \
     {                                                                                                  \
         return launch_dd<k>(solve, P, smem, st);                                                       \
     }
 #define ALIP_LAUNCH_DECL(k)                                                                            \
-    hipError_t launch_lip_##k(bool solve, bool f32, const KP& P, size_t smem, hipStream_t st);         \
+    hipError_t launch_lip_##k(bool solve, bool f32, const KP& P, size_t smem, hipStream_t st,          \
+                              unsigned* res_out = nullptr);                                            \
     hipError_t launch_dd_##k(bool solve, const KP& P, size_t smem, hipStream_t st);
 ALIP_LAUNCH_DECL(1) ALIP_LAUNCH_DECL(2) ALIP_LAUNCH_DECL(3) ALIP_LAUNCH_DECL(4) ALIP_LAUNCH_DECL(5) ALIP_LAUNCH_DECL(6)
 #if ALIP_PART_N(1)
@@ -3200,6 +3282,11 @@ struct Handle {
     double* dEp = nullptr;
     double* dGu = nullptr;
     double* dEu = nullptr;
+    // work-queue counter pairs of persistent solve launches (a ring: launches in flight on different
+    // streams use different pairs; each pair is reset by the last wave of the launch that used it)
+    static constexpr unsigned NQ = 64;
+    uint32_t* dq = nullptr;
+    mutable unsigned qi = 0;
     // staging for host-pointer calls
     void* stage = nullptr;
     size_t stage_bytes = 0;
@@ -3340,6 +3427,16 @@ size_t smem_bytes(const Handle* h, bool solve)
            (f32 ? sizeof(float) : sizeof(double)) * ((size_t)h->NG * ncp + e + (size_t)WAVES_PER_BLOCK * wsd);
 }
 
+// ALIPMPC_NO_QUEUE=1: one instance per wave for every batch size (A/B of the work-queue launch)
+bool no_queue()
+{
+    static const bool v = [] {
+        const char* e = std::getenv("ALIPMPC_NO_QUEUE");
+        return e && *e && *e != '0';
+    }();
+    return v;
+}
+
 KP make_kp(const Handle* h, long long B, bool solve)
 {
     const alipmpc_cfg& c = h->cfg;
@@ -3377,6 +3474,7 @@ KP make_kp(const Handle* h, long long B, bool solve)
     P.Gu = h->dGu;
     P.Eu = h->dEu;
     P.B = B;
+    if (solve && c.variant != ALIPMPC_VARIANT_DD && !no_queue()) P.queue = h->dq + 2 * (h->qi++ % Handle::NQ);
     return P;
 }
 
@@ -3389,10 +3487,15 @@ int ksm_of(int rows)
     return 1 << 20;
 }
 
-hipError_t launch(const Handle* h, bool solve, const KP& P, hipStream_t st)
+// res_out != null: no launch, report the resident workgroups of the solve kernel (0 for DD: no queue)
+hipError_t launch(const Handle* h, bool solve, const KP& P, hipStream_t st, unsigned* res_out = nullptr)
 {
     const size_t smem = smem_bytes(h, solve);
     const bool f32 = h->cfg.precision == ALIPMPC_PREC_FP32;
+    if (h->cfg.variant == ALIPMPC_VARIANT_DD && res_out) {
+        *res_out = 0;
+        return hipSuccess;
+    }
     if (h->cfg.variant == ALIPMPC_VARIANT_DD) {
         switch (h->N) {
         case 1: return launch_dd_1(solve, P, smem, st);
@@ -3405,12 +3508,12 @@ hipError_t launch(const Handle* h, bool solve, const KP& P, hipStream_t st)
         return hipErrorInvalidValue;
     }
     switch (h->N) {
-    case 1: return launch_lip_1(solve, f32, P, smem, st);
-    case 2: return launch_lip_2(solve, f32, P, smem, st);
-    case 3: return launch_lip_3(solve, f32, P, smem, st);
-    case 4: return launch_lip_4(solve, f32, P, smem, st);
-    case 5: return launch_lip_5(solve, f32, P, smem, st);
-    case 6: return launch_lip_6(solve, f32, P, smem, st);
+    case 1: return launch_lip_1(solve, f32, P, smem, st, res_out);
+    case 2: return launch_lip_2(solve, f32, P, smem, st, res_out);
+    case 3: return launch_lip_3(solve, f32, P, smem, st, res_out);
+    case 4: return launch_lip_4(solve, f32, P, smem, st, res_out);
+    case 5: return launch_lip_5(solve, f32, P, smem, st, res_out);
+    case 6: return launch_lip_6(solve, f32, P, smem, st, res_out);
     }
     return hipErrorInvalidValue;
 }
@@ -3580,6 +3683,8 @@ int alipmpc_create(const alipmpc_cfg* cfg, int device, void** handle)
                hipMemcpy(*d, v.data(), v.size() * sizeof(double), hipMemcpyHostToDevice) == hipSuccess;
     };
     if (!up(&h->dGp, Gp) || !up(&h->dEp, Ep) || !up(&h->dGu, Gu) || !up(&h->dEu, Eu) ||
+        hipMalloc(&h->dq, 2 * Handle::NQ * sizeof(uint32_t)) != hipSuccess ||
+        hipMemset(h->dq, 0, 2 * Handle::NQ * sizeof(uint32_t)) != hipSuccess ||
         hipStreamCreateWithFlags(&h->own, hipStreamNonBlocking) != hipSuccess ||
         !create_events(h)) {
         alipmpc_destroy(h);
@@ -3950,6 +4055,18 @@ const char* alipmpc_last_error(void* handle)
     return h ? h->err.c_str() : "null handle";
 }
 
+int alipmpc_solve_slots(void* handle, int64_t* slots)
+{
+    Handle* h = (Handle*)handle;
+    if (!h || !slots) return fail(h, ALIPMPC_EINVAL, "null argument");
+    HIPCHK(h, hipSetDevice(h->device));
+    unsigned res = 0;
+    KP P = make_kp(h, 1, true);
+    HIPCHK(h, launch(h, true, P, h->own, &res));
+    *slots = (int64_t)res * WAVES_PER_BLOCK;
+    return ALIPMPC_OK;
+}
+
 void alipmpc_destroy(void* handle)
 {
     Handle* h = (Handle*)handle;
@@ -3958,6 +4075,7 @@ void alipmpc_destroy(void* handle)
     if (h->own) hipStreamSynchronize(h->own);
     for (double* d : {h->dGp, h->dEp, h->dGu, h->dEu})
         if (d) (void)hipFree(d);
+    if (h->dq) hipFree(h->dq);
     if (h->stage) hipFree(h->stage);
     if (h->rstage) hipFree(h->rstage);
     for (auto& pr : h->ev)
