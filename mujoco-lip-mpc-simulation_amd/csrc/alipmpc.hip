@@ -1325,6 +1325,7 @@ __device__ __forceinline__ void solve_one(const KP& P, R* G, R* E, R* wsb, int w
     int nf = 0;
     R dw_last = R(0.0);
     int status = -1, it = 0, n_rest = 0;
+    int fail_it = -1, it_end = max_iter;   // Error_In_Step_Computation: iteration, and the loop's end
     R e0 = INFINITY;
     const R gth = R(1e-5), gph = R(1e-8), sth = R(1.1), sph = R(2.3), eta = R(1e-8), gal = R(0.05);
 
@@ -1420,7 +1421,7 @@ __device__ __forceinline__ void solve_one(const KP& P, R* G, R* E, R* wsb, int w
                 status = 0;
                 break;
             }
-            if (it == max_iter) break;
+            if (it >= it_end) break;
             const R mu_min = w.cst[K_TOL] / R(10.0);
             const R mu_prev = mu;
             for (int t = 0; t < 8; ++t) {
@@ -1441,7 +1442,7 @@ __device__ __forceinline__ void solve_one(const KP& P, R* G, R* E, R* wsb, int w
             break;
         }
         STAMP(2);
-        if (status == 0 || it == max_iter) break;
+        if (status == 0 || it >= it_end) break;
         const R tau = uni(fmax(R(0.99), R(1.0) - mu));
 
         // ---- Sigma, rhs weights, Hessian blocks
@@ -1630,14 +1631,17 @@ __device__ __forceinline__ void solve_one(const KP& P, R* G, R* E, R* wsb, int w
 #pragma unroll
             for (int j = 0; j < n; ++j)
                 v += G[(lane < NG ? lane : 0) * NCP + j] * (GJ ? w.S[j * GJLD + n] : bcast(xv, j));
-            dvme = lane < NG ? v : R(0.0);
+            // a factorisation the regularisation could not rescue: zero step (the iterate stays), and the
+            // solve ends at the next iteration's test with status -3 (no extra loop exit here: an exit
+            // edge in mid-iteration lengthens live ranges and costs spills)
+            dvme = lane < NG && fact_ok ? v : R(0.0);
             if (lane < NG) w.dV[lane] = dvme;
         }
         wave_sync();
         if constexpr (GJ) gj_zero<n, GJLD>(w.S, lane);   // hess_blocks writes only the nonzero pattern of S
-        if (!fact_ok) {   // keep the last iterate (dV is scratch; V untouched)
-            status = -3;
-            break;
+        if (!fact_ok && fail_it < 0) {
+            fail_it = it;
+            it_end = it + 1;
         }
         // ---- slack / multiplier steps, fraction to boundary
         RELANE();
@@ -1835,6 +1839,10 @@ __device__ __forceinline__ void solve_one(const KP& P, R* G, R* E, R* wsb, int w
     }
     STAMP(8);
     STAMP_FLUSH;
+    if (fail_it >= 0) {   // the last iterate, as IPOPT returns it with Error_In_Step_Computation
+        status = -3;
+        it = fail_it;
+    }
     // ---- status + outputs (violation measured on the reference's exact |.|)
     wave_sync();
     RELANE();
