@@ -1165,12 +1165,14 @@ __device__ void hess_blocks(const WSS<N, R>& w, int lane, int rps, int nobs, int
 //   MFMA KKT products.
 // ------------------------------------------------------------------------------------------------
 template <int N, int KSM, class R, bool Q>
-__device__ __forceinline__ void solve_one(const KP& P, R* G, R* E, R* wsb, int wv, long long b)
+__device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int wv, long long b)
 {
     // Q (persistent instance loop): opaque per-instance copies of the lane-/wave-derived inputs, so that
     // nothing computed from them is loop-invariant and no address or row table is hoisted out of the
-    // instance loop (and spilled)
+    // instance loop (and spilled).  (Laundering the LDS base offsets as well cut the scratch further but
+    // measured slower: profiles/r1f/ab_occupancy.log.)
     if constexpr (Q) asm volatile("" : "+s"(wv), "+s"(b));
+    const KP& P = P0;
     using D = Dim<N>;
     constexpr int n = D::n;
     constexpr int NT = D::NT;
@@ -1898,8 +1900,21 @@ __device__ __forceinline__ void queue_exit(uint32_t* q)
     }
 }
 
+#ifndef ALIP_WAVES_RPL1
+#define ALIP_WAVES_RPL1 4
+#endif
+#ifndef ALIP_WAVES_RPL2
+#define ALIP_WAVES_RPL2 2
+#endif
+// waves per SIMD the register budget is sized for (512 / waves VGPRs per lane).  One row group per lane
+// (RPL = 1): 4 waves, 128 VGPRs, a few spilled values.  Two row groups (RPL = 2, N >= 4 or many
+// obstacles): the row state alone is ~110 VGPRs, and at 128 VGPRs it spilled 400 B/lane; 2 waves with
+// 256 VGPRs spill nothing and measured +48 % on cfg3 (profiles/r1f/ab_occupancy.log)
+template <int KSM>
+constexpr int solve_waves() { return 4 * KSM > WAVE ? ALIP_WAVES_RPL2 : ALIP_WAVES_RPL1; }
+
 template <int N, int KSM, class R, bool QUEUE>
-__global__ __launch_bounds__(256, 4) void solve_kernel(KP Pv)
+__global__ __launch_bounds__(256, solve_waves<KSM>()) void solve_kernel(KP Pv)
 {
     using D = Dim<N>;
     constexpr int NCP = D::NCP;
