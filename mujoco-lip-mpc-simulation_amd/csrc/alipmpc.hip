@@ -2404,8 +2404,20 @@ __device__ double dd_hess_entry(const DDW<N>& w, const double* ST, int a, int b)
 // ------------------------------------------------------------------------------------------------
 // DD solve kernel (one instance per wave); RPL row groups of 64 lanes, KSM = 16 RPL J-layout steps
 // ------------------------------------------------------------------------------------------------
+// DD solve kernels: 2 waves per SIMD (256 VGPRs).  At 4 waves they spilled 132 / 244 / 356 B per lane
+// (RPL = 1 / 2 / 3); at 2 waves: N = 3, 5 circles +11 %, N = 5, 5 + 5 obstacles 2.0x
+// (profiles/r1f/ab_dd_occupancy.log)
+#ifndef ALIP_DD_WAVES_RPL1
+#define ALIP_DD_WAVES_RPL1 2
+#endif
+#ifndef ALIP_DD_WAVES_RPL2
+#define ALIP_DD_WAVES_RPL2 2
+#endif
+template <int RPL>
+constexpr int dd_solve_waves() { return RPL > 1 ? ALIP_DD_WAVES_RPL2 : ALIP_DD_WAVES_RPL1; }
+
 template <int N, int RPL>
-__global__ __launch_bounds__(256, 4) void dd_solve_kernel(KP Pv)
+__global__ __launch_bounds__(256, dd_solve_waves<RPL>()) void dd_solve_kernel(KP Pv)
 {
     constexpr int n = 2 * N;
     constexpr int KSM = 16 * RPL;
