@@ -1910,11 +1910,17 @@ __device__ __forceinline__ void queue_exit(uint32_t* q)
 // (RPL = 1): 4 waves, 128 VGPRs, a few spilled values.  Two row groups (RPL = 2, N >= 4 or many
 // obstacles): the row state alone is ~110 VGPRs, and at 128 VGPRs it spilled 400 B/lane; 2 waves with
 // 256 VGPRs spill nothing and measured +48 % on cfg3 (profiles/r1f/ab_occupancy.log)
-template <int KSM>
-constexpr int solve_waves() { return 4 * KSM > WAVE ? ALIP_WAVES_RPL2 : ALIP_WAVES_RPL1; }
+// fp32, one row group: 93-103 VGPRs at 4 waves; 7 waves (72 VGPRs, some spills in the queue kernel)
+// measured best on cfg5: 4 -> 5 -> 6 -> 7 -> 8 waves = 21.0 / 21.9 / 22.7 / 23.1 / 22.1 M solves/s
+// (profiles/r1f/ab_fp32_occupancy.log)
+#ifndef ALIP_WAVES_F32
+#define ALIP_WAVES_F32 7
+#endif
+template <int KSM, class R>
+constexpr int solve_waves() { return 4 * KSM > WAVE ? ALIP_WAVES_RPL2 : (sizeof(R) == 4 ? ALIP_WAVES_F32 : ALIP_WAVES_RPL1); }
 
 template <int N, int KSM, class R, bool QUEUE>
-__global__ __launch_bounds__(256, solve_waves<KSM>()) void solve_kernel(KP Pv)
+__global__ __launch_bounds__(256, (solve_waves<KSM, R>())) void solve_kernel(KP Pv)
 {
     using D = Dim<N>;
     constexpr int NCP = D::NCP;
