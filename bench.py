@@ -114,7 +114,6 @@ def main():
         from alipmpc import sharding
         lo, hi = sharding.shard_range(preset["batch"], rank, world)
         B = hi - lo
-    B_cap = -(-preset["batch"] // world) if not (preset["per_gpu"] or args.batch is not None) else B
     prec = {"precision": alipmpc.PREC_FP32} if fp32 else {}
     cfg = alipmpc.default_cfg(variant, N, nc_max=n_cir, ne_max=n_elp, **prec)
     solver = alipmpc.Solver(cfg, device=dev.index)
@@ -143,53 +142,17 @@ def main():
         "status": torch.empty((B,), dtype=torch.int32, device=dev),
         "iters": torch.empty((B,), dtype=torch.int32, device=dev),
     }
-    # one gather of per-instance outputs (u, foot, status, iters packed as fp64 rows) to rank 0
-    # (padded to the largest shard so every rank contributes the same shape)
-    pack_w = n + 3 + 2
-    packed = torch.zeros((B_cap, pack_w), dtype=torch.float64, device=dev)
-    gathered = [torch.empty_like(packed) for _ in range(world)] if (world > 1 and rank == 0) else None
+    # one gather of the per-instance outputs (u, foot, status, iters packed as fp64 rows) to rank 0 per
+    # step: sharding.gather_to_root (the collective the gloo tests cover), padded to the largest shard
     stream = torch.cuda.current_stream(dev)
-
-    def pack_and_gather():
-        packed[:B, :n] = out["u"]
-        packed[:B, n:n + 3] = out["foot"]
-        packed[:B, n + 3] = out["status"].to(torch.float64)
-        packed[:B, n + 4] = out["iters"].to(torch.float64)
-        dist.gather(packed, gathered, dst=0)
-
-    def step():
-        solver.solve_device(inp, out, stream=stream)
-        if world > 1:
-            pack_and_gather()
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
+    solve = lambda: solver.solve_device(inp, out, stream=stream)  # noqa: E731
+    step = make_step(solve, out, n, B_total_of(preset, args, B, world), rank, world, stream)
+    elapsed, ev = timed_loop(step, args.warmup, args.steps, world, dev)
     K = args.steps
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for k in range(K):
-        ev[k][0].record(stream)
-        solver.solve_device(inp, out, stream=stream)
-        ev[k][1].record(stream)
-        if world > 1:
-            pack_and_gather()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     status = out["status"].cpu().numpy()
     iters = out["iters"].cpu().numpy()
-    B_total = B * world if (preset["per_gpu"] or args.batch is not None) else preset["batch"]
+    B_total = B_total_of(preset, args, B, world)
     total_solves = B_total * K
     value = total_solves / elapsed
     # roofline of the dominant kernel (solve_kernel): algorithmic FP64 flops per launch / launch time
@@ -214,7 +177,9 @@ def main():
         except Exception:
             traffic = None
 
-    feas = feasible_fraction(alipmpc, solver, cfg, inp, out, dev, world, dist) if fp32 else None
+    # quality beside the rate (every config): solves/s counts every instance, so report how many of them
+    # converged and how many returned plans are feasible for the reference constraints
+    feas = feasible_fraction(alipmpc, solver, cfg, inp, out, dev, world, dist)
 
     sweep = jacobian_sweep(alipmpc, scenes, variant, args, dev) if (rank == 0 and args.sweep_batch > 0) else None
 
@@ -272,6 +237,68 @@ def main():
         dist.destroy_process_group()
 
 
+def B_total_of(preset, args, B, world):
+    """Instances in the whole job: per-GPU configs (weak scaling) B x world; fixed totals (strong) the
+    config's batch."""
+    return B * world if (preset["per_gpu"] or args.batch is not None) else preset["batch"]
+
+
+def pack_outputs(out, n):
+    """Per-instance outputs as fp64 rows [u (n) | foot (3) | status | iters] (the gathered record)."""
+    import torch
+    return torch.cat([out["u"].reshape(-1, n), out["foot"], out["status"].to(torch.float64).reshape(-1, 1),
+                      out["iters"].to(torch.float64).reshape(-1, 1)], dim=1)
+
+
+def make_step(solve, out, n, B_total, rank, world, stream=None):
+    """One bench step: the solve launch (bracketed by the given HIP event pair, recorded on the launch
+    stream), then at N > 1 one gather of the packed outputs to rank 0 with alipmpc.sharding.gather_to_root
+    (contiguous shards of B_total, padded to the largest).  step(ev) returns the gathered
+    [B_total, n + 5] tensor on rank 0 (None on the other ranks and at N = 1)."""
+    from alipmpc import sharding
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        solve()
+        if ev is not None:
+            ev[1].record(stream)
+        if world == 1:
+            return None
+        return sharding.gather_to_root(pack_outputs(out, n), B_total, rank, world)
+    return step
+
+
+def timed_loop(step, warmup, K, world, dev):
+    """W untimed steps, then K timed steps bracketed by barrier + synchronize on both sides; returns the
+    max-over-ranks wall time and the per-launch HIP event pairs (none on a CPU device: the gloo tests
+    drive this loop with a stub solver)."""
+    import torch
+    import torch.distributed as dist
+    gpu = torch.device(dev).type == "cuda"
+    sync = (lambda: torch.cuda.synchronize(dev)) if gpu else (lambda: None)  # noqa: E731
+    for _ in range(warmup):
+        step()
+    sync()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if gpu else None
+          for _ in range(K)]
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for k in range(K):
+        step(ev[k])
+    sync()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, ev
+
+
 def jacobian_sweep(alipmpc, scenes, variant, args, dev, reps=10):
     """HBM roofline of the unfused Jacobian sweep (eval_kernel: f, grad f, c, J of the
     reference callbacks at given u) on cfg2-shaped instances (N = 3, 5 circles) whatever --config is.
@@ -311,9 +338,9 @@ def jacobian_sweep(alipmpc, scenes, variant, args, dev, reps=10):
 
 
 def feasible_fraction(alipmpc, solver, cfg, inp, out, dev, world, dist, chunk=65536):
-    """cfg5: share of instances whose solution u, evaluated by the fp64 eval kernel (the reference
-    callbacks), violates no active constraint row by more than 1e-4 (the reference analogue is
-    status != 2, 86.6 % in its logs).  Also the share with status 0 or 1.  Counts are summed over ranks."""
+    """Share of instances whose returned u, evaluated by the fp64 eval kernel (the reference callbacks),
+    violates no active constraint row by more than 1e-4 (the reference analogue is status != 2,
+    86.6 % in its logs), and the shares with status 0 or 1 / status 0.  Counts are summed over ranks."""
     import torch
     c64 = alipmpc.default_cfg(cfg.variant, cfg.N, nc_max=cfg.nc_max, ne_max=cfg.ne_max)
     ev = alipmpc.Solver(c64, device=dev.index)
@@ -332,14 +359,23 @@ def feasible_fraction(alipmpc, solver, cfg, inp, out, dev, world, dist, chunk=65
         v = torch.clamp(torch.maximum(o["cl"] - o["c"], o["c"] - o["cu"]), min=0.0)
         v = torch.where(o["row_active"] != 0, v, torch.zeros_like(v))
         feas += int((v.amax(dim=1) <= 1e-4).sum().item())
-    st = out["status"]
-    conv = int(((st == 0) | (st == 1)).sum().item())
-    cnt = torch.tensor([feas, conv, B], dtype=torch.float64, device=dev)
+    return quality_counts(feas, out["status"], dev, world)
+
+
+def quality_counts(feas, status, dev, world):
+    """Feasible / converged (status 0 or 1) / solved (status 0) shares over the whole job: per-rank counts
+    summed with one all-reduce."""
+    import torch
+    import torch.distributed as dist
+    conv = int(((status == 0) | (status == 1)).sum().item())
+    solved = int((status == 0).sum().item())
+    cnt = torch.tensor([feas, conv, solved, status.numel()], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(cnt)
-    feas, conv, tot = (float(x) for x in cnt.tolist())
-    return {"feasible_fraction": feas / tot, "converged_fraction": conv / tot, "instances": int(tot),
-            "check": "fp64 reference callbacks at the fp32 solution, max active-row violation <= 1e-4"}
+    feas, conv, solved, tot = (float(x) for x in cnt.tolist())
+    return {"feasible_fraction": feas / tot, "converged_fraction": conv / tot, "solved_fraction": solved / tot,
+            "instances": int(tot),
+            "check": "fp64 reference callbacks at the returned u, max active-row violation <= 1e-4"}
 
 
 def cpu_baseline(cfg, batch, seconds, threads=1, workload="cfg2"):

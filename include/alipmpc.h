@@ -24,6 +24,11 @@
  *     is asynchronous on that stream (no host synchronisation, no allocation after the first call of a
  *     given batch size — graph-capturable).  ALIPMPC_STREAM_NULL selects device pointers on the null
  *     (default) stream, whose handle value is 0.
+ *   - Every LIP solve launch takes one of the handle's 64 work-queue counter pairs (a ring; each pair is
+ *     reset by the last wave of the launch that used it).  A solve captured into a hipGraph bakes in one
+ *     pair: do not replay such a graph concurrently with itself, and keep fewer than 64 solve launches of
+ *     one handle in flight at once (across all streams), or two launches share counters and instances
+ *     are skipped or solved twice.
  *   - Row-major, instance-major arrays ("B x k" = k contiguous values per instance).
  *   - Return 0 on success, a negative ALIPMPC_E* code on error; alipmpc_last_error(h) gives the text.
  *   - There is no CPU execution path: a handle needs a visible gfx950 device.
@@ -85,7 +90,10 @@ typedef struct alipmpc_cfg {
     int32_t ne_max;     /* ellipse slots per instance */
     int32_t variant;    /* ALIPMPC_VARIANT_* */
     int32_t max_iter;   /* interior-point iteration cap */
-    int32_t precision;  /* ALIPMPC_PREC_FP64 / _FP32 (device arithmetic; host buffers stay fp64) */
+    int32_t precision;  /* ALIPMPC_PREC_FP64 / _FP32 (device arithmetic; host buffers stay fp64).  With
+                           FP32 and tol / acceptable_tol still at the fp64 defaults (1e-8 / 1e-6, below
+                           fp32 resolution), alipmpc_create uses the fp32 defaults: 1e-4 / 1e-3 for
+                           N <= 3, 3e-4 / 3e-3 for N > 3 */
     int32_t select_obs; /* 1: MPCCBF.select_obs range filter (modi) */
     int32_t detour;     /* 1: local-goal detour heuristic of solveMPCCBF (modi, sig_step) */
     double tol;         /* overall KKT tolerance (IPOPT tol, default 1e-8) */
@@ -197,11 +205,11 @@ int alipmpc_trace_batch(void* handle, int64_t B, const double* x0, const double*
                         void* hip_stream);
 
 /* Instances this handle's solve kernel holds resident on its device at once (resident workgroups x 4
- * waves, one instance per wave).  A solve_batch / rollout with more instances than this runs a persistent
- * grid of exactly the resident workgroups that pulls instances from a per-launch work queue (a wave that
- * finishes a short solve takes the next instance); smaller batches launch one wave per instance.  The
- * per-instance results do not depend on the launch form.  0 for the DD variant (always one wave per
- * instance).  No reference counterpart (scheduling of the batched replacement). */
+ * waves, one instance per wave).  Every LIP solve / rollout launch is a persistent grid of at most the
+ * resident workgroups whose waves pull instances from a per-launch work queue (a wave that finishes a
+ * short solve takes the next instance), so one program solves every batch size and an instance's result
+ * does not depend on B (a batch solved whole or in chunks is bit-identical).  0 for the DD variant
+ * (always one wave per instance).  No reference counterpart (scheduling of the batched replacement). */
 int alipmpc_solve_slots(void* handle, int64_t* slots);
 
 /* Duration in milliseconds of the most recent solve kernel launch on this handle, measured with HIP

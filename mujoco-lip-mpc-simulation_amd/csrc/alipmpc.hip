@@ -24,6 +24,7 @@
 //     line search; same algorithm and constants as oracle/np_oracle.py and oracle/alipmpc_oracle.c.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -1919,7 +1920,12 @@ __device__ __forceinline__ void queue_exit(uint32_t* q)
 template <int KSM, class R>
 constexpr int solve_waves() { return 4 * KSM > WAVE ? ALIP_WAVES_RPL2 : (sizeof(R) == 4 ? ALIP_WAVES_F32 : ALIP_WAVES_RPL1); }
 
-template <int N, int KSM, class R, bool QUEUE>
+// One program per configuration: every solve launch is a grid of at most the resident workgroups whose
+// waves take instances from the launch's work queue, whatever the batch size.  An instance's arithmetic
+// therefore does not depend on B or on the device's slot count (a batch solved whole or in chunks gives
+// bit-identical results), and a wave that finishes a short solve takes the next instance at once instead
+// of idling until its workgroup's longest solve ends (a workgroup's slots are only refilled as a whole).
+template <int N, int KSM, class R>
 __global__ __launch_bounds__(256, (solve_waves<KSM, R>())) void solve_kernel(KP Pv)
 {
     using D = Dim<N>;
@@ -1936,19 +1942,10 @@ __global__ __launch_bounds__(256, (solve_waves<KSM, R>())) void solve_kernel(KP 
     __syncthreads();
     const KP& P = *Ps;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);   // wave-uniform (SGPR)
-    // QUEUE = false: one instance per wave.  QUEUE = true (more instances than resident wave slots): a
-    // persistent grid of the resident workgroups pulls instances from the launch's work queue, so that a
-    // wave that finishes a short solve takes the next instance instead of idling until its workgroup's
-    // longest solve ends (a workgroup's slots are only refilled as a whole)
-    if constexpr (!QUEUE) {
-        const long long b = (long long)blockIdx.x * WAVES_PER_BLOCK + wv;
-        if (b < Pv.B && (!Pv.active || Pv.active[b])) solve_one<N, KSM, R, false>(P, G, E, wsb, wv, b);
-    } else {
-        uint32_t* const q = Pv.queue;
-        for (long long b = next_instance(q); b < Pv.B; b = next_instance(q))
-            if (!Pv.active || Pv.active[b]) solve_one<N, KSM, R, true>(P, G, E, wsb, wv, b);   // rollout: skip finished
-        queue_exit(q);
-    }
+    uint32_t* const q = Pv.queue;
+    for (long long b = next_instance(q); b < Pv.B; b = next_instance(q))
+        if (!Pv.active || Pv.active[b]) solve_one<N, KSM, R, true>(P, G, E, wsb, wv, b);   // rollout: skip finished
+    queue_exit(q);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -3196,41 +3193,32 @@ template <int N, class R>
 void launch_solve(const KP& P0, size_t smem, hipStream_t st, unsigned* res_out)
 {
     const unsigned need = (unsigned)((P0.B + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
-    {
-        // KSM = 4-row steps of the J layout, the smallest compiled size covering mo4 rows
-        auto go = [&](auto kern, auto kern_q) {
-            // more instances than resident wave slots: a persistent grid of exactly the resident
-            // workgroups pulls instances from the work queue; otherwise one instance per wave
-            set_smem((const void*)kern_q, smem);
-            const unsigned res = resident_blocks((const void*)kern_q, smem);
-            if (res_out) {   // query only (alipmpc_solve_slots)
-                *res_out = res;
-                return;
-            }
-            if (P0.queue && res > 0 && need > res && P0.B < (1LL << 31)) {
-                hipLaunchKernelGGL(kern_q, dim3(res), dim3(WAVE * WAVES_PER_BLOCK), smem, st, P0);
-            } else {
-                KP P = P0;
-                P.queue = nullptr;
-                set_smem((const void*)kern, smem);
-                hipLaunchKernelGGL(kern, dim3(need), dim3(WAVE * WAVES_PER_BLOCK), smem, st, P);
-            }
-        };
-        if (P0.mo4 <= 32)
-            go(solve_kernel<N, 8, R, false>, solve_kernel<N, 8, R, true>);
-        else if (P0.mo4 <= 40)
-            go(solve_kernel<N, 10, R, false>, solve_kernel<N, 10, R, true>);
-        else if (P0.mo4 <= 48)
-            go(solve_kernel<N, 12, R, false>, solve_kernel<N, 12, R, true>);
-        else if (P0.mo4 <= 64)
-            go(solve_kernel<N, 16, R, false>, solve_kernel<N, 16, R, true>);
-        else if (P0.mo4 <= 96)
-            go(solve_kernel<N, 24, R, false>, solve_kernel<N, 24, R, true>);
-        else if (P0.mo4 <= 128)
-            go(solve_kernel<N, 32, R, false>, solve_kernel<N, 32, R, true>);
-        else
-            go(solve_kernel<N, 48, R, false>, solve_kernel<N, 48, R, true>);
-    }
+    // KSM = 4-row steps of the J layout, the smallest compiled size covering mo4 rows
+    auto go = [&](auto kern) {
+        set_smem((const void*)kern, smem);
+        const unsigned res = resident_blocks((const void*)kern, smem);
+        if (res_out) {   // query only (alipmpc_solve_slots)
+            *res_out = res;
+            return;
+        }
+        // a persistent grid of at most the resident workgroups (the work queue hands out the instances)
+        const unsigned grid = res > 0 && res < need ? res : need;
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(WAVE * WAVES_PER_BLOCK), smem, st, P0);
+    };
+    if (P0.mo4 <= 32)
+        go(solve_kernel<N, 8, R>);
+    else if (P0.mo4 <= 40)
+        go(solve_kernel<N, 10, R>);
+    else if (P0.mo4 <= 48)
+        go(solve_kernel<N, 12, R>);
+    else if (P0.mo4 <= 64)
+        go(solve_kernel<N, 16, R>);
+    else if (P0.mo4 <= 96)
+        go(solve_kernel<N, 24, R>);
+    else if (P0.mo4 <= 128)
+        go(solve_kernel<N, 32, R>);
+    else
+        go(solve_kernel<N, 48, R>);
 }
 
 // solve kernels run in the handle's precision (cfg.precision); the eval hook is always fp64
@@ -3327,7 +3315,7 @@ struct Handle {
     // streams use different pairs; each pair is reset by the last wave of the launch that used it)
     static constexpr unsigned NQ = 64;
     uint32_t* dq = nullptr;
-    mutable unsigned qi = 0;
+    mutable std::atomic<unsigned> qi{0};
     // staging for host-pointer calls
     void* stage = nullptr;
     size_t stage_bytes = 0;
@@ -3468,16 +3456,6 @@ size_t smem_bytes(const Handle* h, bool solve)
            (f32 ? sizeof(float) : sizeof(double)) * ((size_t)h->NG * ncp + e + (size_t)WAVES_PER_BLOCK * wsd);
 }
 
-// ALIPMPC_NO_QUEUE=1: one instance per wave for every batch size (A/B of the work-queue launch)
-bool no_queue()
-{
-    static const bool v = [] {
-        const char* e = std::getenv("ALIPMPC_NO_QUEUE");
-        return e && *e && *e != '0';
-    }();
-    return v;
-}
-
 KP make_kp(const Handle* h, long long B, bool solve)
 {
     const alipmpc_cfg& c = h->cfg;
@@ -3515,7 +3493,7 @@ KP make_kp(const Handle* h, long long B, bool solve)
     P.Gu = h->dGu;
     P.Eu = h->dEu;
     P.B = B;
-    if (solve && c.variant != ALIPMPC_VARIANT_DD && !no_queue()) P.queue = h->dq + 2 * (h->qi++ % Handle::NQ);
+    if (solve && c.variant != ALIPMPC_VARIANT_DD) P.queue = h->dq + 2 * (h->qi.fetch_add(1u) % Handle::NQ);
     return P;
 }
 
@@ -3685,6 +3663,12 @@ int alipmpc_create(const alipmpc_cfg* cfg, int device, void** handle)
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return ALIPMPC_ENODEV;
     Handle* h = new Handle();
     h->cfg = *cfg;
+    if (cfg->precision == ALIPMPC_PREC_FP32 && cfg->tol == 1e-8 && cfg->acceptable_tol == 1e-6) {
+        // the fp64 defaults are below fp32 resolution: use the horizon-aware fp32 defaults (the ctypes
+        // layer's FP32_TOL*); N > 3 decision-space gradients grow through A^k and lift the fp32 floor
+        h->cfg.tol = cfg->N > 3 ? 3e-4 : 1e-4;
+        h->cfg.acceptable_tol = cfg->N > 3 ? 3e-3 : 1e-3;
+    }
     h->device = device;
     h->N = cfg->N;
     h->n = 3 * cfg->N;
@@ -3753,6 +3737,7 @@ static int run_batch(Handle* h, bool solve, int64_t B, const double* x0, const d
     if (!x0 || !goal || (!leg && !dd) || !nc || !u0 || (cf.nc_max > 0 && !cir) || (cf.ne_max > 0 && (!elp || !ne)))
         return fail(h, ALIPMPC_EINVAL, "missing input pointer");
     if (solve && !u_out) return fail(h, ALIPMPC_EINVAL, "u_out is required");
+    if (solve && B >= (int64_t)1 << 31) return fail(h, ALIPMPC_EINVAL, "B >= 2^31 (32-bit work-queue counter)");
     HIPCHK(h, hipSetDevice(h->device));
     // host-facing u: the reference's 5N-vector (LIP) / 2N controls (DD); state dimension 5 / 3
     const int N = h->N, n = dd ? 2 * N : 5 * N, sd = dd ? 3 : 5;
@@ -3774,44 +3759,57 @@ static int run_batch(Handle* h, bool solve, int64_t B, const double* x0, const d
         h->timed = true;
         return ALIPMPC_OK;
     }
-    // host pointers: stage through the handle's device workspace
+    // host pointers: stage through the handle's device workspace (only the regions this call uses: the
+    // solve outputs for a solve, the eval outputs for an eval, J only when it is requested)
     const size_t Bz = (size_t)B;
+    struct Stage {
+        double *x0, *goal, *cir, *elp, *u0, *lu, *u, *foot, *xp, *f, *g, *c, *J, *cl, *cu, *ge;
+        int8_t *leg, *ra;
+        int32_t *nc, *ne, *st, *it;
+    };
+    auto carve = [&](Carver& cv) {
+        Stage z{};
+        z.x0 = cv.take<double>(Bz * sd);
+        z.goal = cv.take<double>(Bz * 2);
+        z.leg = cv.take<int8_t>(Bz);
+        z.cir = cv.take<double>(Bz * 3 * cf.nc_max);
+        z.nc = cv.take<int32_t>(Bz);
+        z.elp = cv.take<double>(Bz * 5 * cf.ne_max);
+        z.ne = cv.take<int32_t>(Bz);
+        z.u0 = cv.take<double>(Bz * n);
+        z.lu = cv.take<double>(Bz * 2);
+        if (solve) {
+            z.u = cv.take<double>(Bz * n);
+            z.foot = cv.take<double>(Bz * 3);
+            z.xp = cv.take<double>(Bz * sd * N);
+            z.st = cv.take<int32_t>(Bz);
+            z.it = cv.take<int32_t>(Bz);
+        } else {
+            z.f = cv.take<double>(Bz);
+            z.g = cv.take<double>(Bz * n);
+            z.c = cv.take<double>(Bz * mm_);
+            if (J) z.J = cv.take<double>(Bz * mm_ * n);
+            z.cl = cv.take<double>(Bz * mm_);
+            z.cu = cv.take<double>(Bz * mm_);
+            z.ge = cv.take<double>(Bz * 2);
+            z.ra = cv.take<int8_t>(Bz * mm_);
+        }
+        return z;
+    };
     size_t need = 0;
     {
         Carver cv{nullptr};
-        cv.take<double>(Bz * sd); cv.take<double>(Bz * 2); cv.take<int8_t>(Bz); cv.take<double>(Bz * 3 * cf.nc_max);
-        cv.take<int32_t>(Bz); cv.take<double>(Bz * 5 * cf.ne_max); cv.take<int32_t>(Bz); cv.take<double>(Bz * n);
-        cv.take<double>(Bz * 2);
-        cv.take<double>(Bz * n); cv.take<double>(Bz * 3); cv.take<double>(Bz * sd * N); cv.take<int32_t>(Bz);
-        cv.take<int32_t>(Bz); cv.take<double>(Bz); cv.take<double>(Bz * n); cv.take<double>(Bz * mm_);
-        cv.take<double>(Bz * mm_ * n); cv.take<double>(Bz * mm_); cv.take<double>(Bz * mm_); cv.take<double>(Bz * 2);
-        cv.take<int8_t>(Bz * mm_);
+        carve(cv);
         need = cv.off + 256;
     }
     if (int e = ensure_stage(h, need)) return e;
     Carver cv{(char*)h->stage};
-    double* d_x0 = cv.take<double>(Bz * sd);
-    double* d_goal = cv.take<double>(Bz * 2);
-    int8_t* d_leg = cv.take<int8_t>(Bz);
-    double* d_cir = cv.take<double>(Bz * 3 * cf.nc_max);
-    int32_t* d_nc = cv.take<int32_t>(Bz);
-    double* d_elp = cv.take<double>(Bz * 5 * cf.ne_max);
-    int32_t* d_ne = cv.take<int32_t>(Bz);
-    double* d_u0 = cv.take<double>(Bz * n);
-    double* d_lu = cv.take<double>(Bz * 2);
-    double* d_u = cv.take<double>(Bz * n);
-    double* d_foot = cv.take<double>(Bz * 3);
-    double* d_xp = cv.take<double>(Bz * sd * N);
-    int32_t* d_st = cv.take<int32_t>(Bz);
-    int32_t* d_it = cv.take<int32_t>(Bz);
-    double* d_f = cv.take<double>(Bz);
-    double* d_g = cv.take<double>(Bz * n);
-    double* d_c = cv.take<double>(Bz * mm_);
-    double* d_J = cv.take<double>(Bz * mm_ * n);
-    double* d_cl = cv.take<double>(Bz * mm_);
-    double* d_cu = cv.take<double>(Bz * mm_);
-    double* d_ge = cv.take<double>(Bz * 2);
-    int8_t* d_ra = cv.take<int8_t>(Bz * mm_);
+    const Stage z = carve(cv);
+    double *d_x0 = z.x0, *d_goal = z.goal, *d_cir = z.cir, *d_elp = z.elp, *d_u0 = z.u0, *d_lu = z.lu;
+    double *d_u = z.u, *d_foot = z.foot, *d_xp = z.xp, *d_f = z.f, *d_g = z.g, *d_c = z.c, *d_J = z.J;
+    double *d_cl = z.cl, *d_cu = z.cu, *d_ge = z.ge;
+    int8_t *d_leg = z.leg, *d_ra = z.ra;
+    int32_t *d_nc = z.nc, *d_ne = z.ne, *d_st = z.st, *d_it = z.it;
     auto h2d = [&](void* d, const void* s, size_t bytes) { return hipMemcpyAsync(d, s, bytes, hipMemcpyHostToDevice, st); };
     auto d2h = [&](void* d, const void* s, size_t bytes) { return hipMemcpyAsync(d, s, bytes, hipMemcpyDeviceToHost, st); };
     HIPCHK(h, h2d(d_x0, x0, Bz * sd * 8));

@@ -493,41 +493,49 @@ def test_fp32_all_horizons_agree_with_fp64(gpu_lib, variant, N):
     assert np.mean(err[both] <= 1e-3) >= 0.9, np.mean(err[both] <= 1e-3)
 
 
-def test_work_queue_launch_matches_per_wave_launch(gpu_lib):
-    """Batches larger than the resident instance slots run the persistent work-queue kernel.  Each
-    instance must come out as it does from the one-wave-per-instance kernel (the same batch solved in
-    chunks that fit the slots), every instance must be solved exactly once (NaN-filled device outputs),
-    and the queue counters must reset between launches (a second launch solves everything again,
-    bit-identically).  A closed-loop rollout (retired instances skipped through the queue) must match
-    its chunked counterpart too."""
+WQ_CASES = [  # (variant, N, circles, ellipses, precision): cfg2/cfg4's kernel, cfg5's (fp32), cfg3's (N = 5)
+    (0, 3, 5, 0, 0), (0, 3, 5, 0, 1), (0, 5, 5, 5, 0)]
+
+
+@pytest.mark.parametrize("variant,N,n_cir,n_elp,prec", WQ_CASES)
+def test_work_queue_batch_independence(gpu_lib, variant, N, n_cir, n_elp, prec):
+    """Every LIP solve launch is the persistent work-queue program (at most the resident workgroups).
+    An instance's result must not depend on the batch it is solved in: the same instances solved as one
+    batch larger than the resident slots and in chunks of half the slots are bit-identical (status, iters,
+    u, foot, x_pred); every instance is solved exactly once (NaN-filled device outputs); the queue counters
+    reset between launches (a second launch reproduces the first bit for bit).  A closed-loop rollout
+    (retired instances skipped through the queue) matches its chunked counterpart bit for bit too."""
     import torch
     from alipmpc import scenes
-    s = gpu_lib.Solver(gpu_lib.default_cfg(0, nc_max=5, ne_max=0))
+    kw = dict(nc_max=n_cir, ne_max=n_elp)
+    if prec:
+        kw["precision"] = gpu_lib.PREC_FP32
+    s = gpu_lib.Solver(gpu_lib.default_cfg(variant, N, **kw))
     slots = s.solve_slots()
     assert slots >= 1024 and slots % 4 == 0, slots
     B = slots + slots // 2 + 37
-    bt = scenes.make_batch(B, seed=71, n_cir=5)
-    big = s.solve(bt["x0"], bt["goal"], bt["leg"], bt["cir"], bt["nc"], u0=bt["u0"])
+    bt = scenes.make_batch_vec(B, seed=71 + N + prec, n_cir=n_cir, n_elp=n_elp, N=N)
+    args = lambda i0, i1: (bt["x0"][i0:i1], bt["goal"][i0:i1], bt["leg"][i0:i1], bt["cir"][i0:i1],  # noqa: E731
+                           bt["nc"][i0:i1], None if bt["elp"] is None else bt["elp"][i0:i1],
+                           None if bt["ne"] is None else bt["ne"][i0:i1])
+    big = s.solve(*args(0, B), u0=bt["u0"])
     ch = slots // 2
-    parts = [s.solve(bt["x0"][i:i + ch], bt["goal"][i:i + ch], bt["leg"][i:i + ch], bt["cir"][i:i + ch],
-                     bt["nc"][i:i + ch], u0=bt["u0"][i:i + ch]) for i in range(0, B, ch)]
+    parts = [s.solve(*args(i, i + ch), u0=bt["u0"][i:i + ch]) for i in range(0, B, ch)]
     small = {k: np.concatenate([p[k] for p in parts]) for k in big}
-    # the two kernels are separately compiled instances of the same source: identical arithmetic per
-    # instance up to the compiler's contraction choices, so require agreement, not bit equality
-    same_status = np.mean(big["status"] == small["status"])
-    both = (big["status"] == 0) & (small["status"] == 0)
-    err = np.abs(big["foot"] - small["foot"]).max(axis=1)
-    assert same_status >= 0.99, same_status
-    assert np.mean(err[both] <= 1e-6) >= 0.99, np.mean(err[both] <= 1e-6)
+    for k in big:
+        assert np.array_equal(big[k], small[k]), k
     dev = torch.device("cuda", 0)
     inp = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in bt.items() if v is not None}
     inp["leg"] = inp["leg"].to(torch.int8)
     inp["nc"] = inp["nc"].to(torch.int32)
+    if "ne" in inp:
+        inp["ne"] = inp["ne"].to(torch.int32)
+    n = 5 * N
     runs = []
     for _ in range(2):
-        out = {"u": torch.full((B, 15), float("nan"), dtype=torch.float64, device=dev),
+        out = {"u": torch.full((B, n), float("nan"), dtype=torch.float64, device=dev),
                "foot": torch.full((B, 3), float("nan"), dtype=torch.float64, device=dev),
-               "x_pred": torch.full((B, 3, 5), float("nan"), dtype=torch.float64, device=dev),
+               "x_pred": torch.full((B, N, 5), float("nan"), dtype=torch.float64, device=dev),
                "status": torch.full((B,), -99, dtype=torch.int32, device=dev),
                "iters": torch.full((B,), -99, dtype=torch.int32, device=dev)}
         s.solve_device(inp, out)
@@ -537,13 +545,140 @@ def test_work_queue_launch_matches_per_wave_launch(gpu_lib):
     for k in runs[0]:
         assert np.array_equal(runs[0][k], runs[1][k]), k
         assert np.array_equal(runs[0][k], big[k]), k
+    if N != 3 or prec:
+        return
     # rollout: queue launch with retired instances vs the same instances in slot-sized chunks
     S = 6
     u0 = np.tile(bt["x0"], (1, 3))
-    r_big = s.rollout(bt["x0"], bt["goal"], bt["leg"], bt["cir"], bt["nc"], u0=u0, steps=S)
-    r_parts = [s.rollout(bt["x0"][i:i + ch], bt["goal"][i:i + ch], bt["leg"][i:i + ch], bt["cir"][i:i + ch],
-                         bt["nc"][i:i + ch], u0=u0[i:i + ch], steps=S) for i in range(0, B, ch)]
+    r_big = s.rollout(*args(0, B), u0=u0, steps=S)
+    r_parts = [s.rollout(*args(i, i + ch), u0=u0[i:i + ch], steps=S) for i in range(0, B, ch)]
     r_small = {k: np.concatenate([p[k] for p in r_parts]) for k in r_big}
-    agree = np.all(np.abs(r_big["foot"] - r_small["foot"]) <= 1e-6, axis=(1, 2))
-    assert agree.mean() >= 0.97, agree.mean()
-    assert np.mean(r_big["steps_to_goal"] == r_small["steps_to_goal"]) >= 0.97
+    for k in r_big:
+        assert np.array_equal(np.nan_to_num(r_big[k], nan=7.0), np.nan_to_num(r_small[k], nan=7.0)), k
+
+
+BENCH_KERNELS = [  # the kernel instance each BASELINE bench number comes from, at B > resident slots
+    ("cfg5", 0, 3, 5, 0, 1), ("cfg3", 0, 5, 5, 5, 0), ("cfg4", 0, 3, 5, 0, 0)]
+
+
+@pytest.mark.parametrize("name,variant,N,n_cir,n_elp,prec", BENCH_KERNELS)
+def test_bench_kernels_beyond_resident_slots_vs_oracle(gpu_lib, coracle, name, variant, N, n_cir, n_elp, prec):
+    """The exact solve program and scene generator bench.py measures for cfg3 / cfg4 / cfg5, at a batch
+    above the resident slots (the persistent work queue cycles every wave through several instances),
+    against the fp64 C oracle on a fixed random subset of 2,048 instances.  Bars: fp64 as
+    test_solve_variants_vs_oracle (cfg3) / test_solve_cfg2_batch_vs_oracle (cfg4); fp32 as
+    test_fp32_solve_vs_oracle (foothold within 1e-3 where both converge)."""
+    from alipmpc import scenes
+    kw = dict(nc_max=n_cir, ne_max=n_elp)
+    if prec:
+        kw["precision"] = gpu_lib.PREC_FP32
+    s = gpu_lib.Solver(gpu_lib.default_cfg(variant, N, **kw))
+    slots = s.solve_slots()
+    B = 2 * slots + 123
+    bt = scenes.make_batch_vec(B, seed=500 + N + 10 * prec, n_cir=n_cir, n_elp=n_elp, N=N,
+                               fields=4096 if name == "cfg3" else None)
+    o = s.solve(bt["x0"], bt["goal"], bt["leg"], bt["cir"], bt["nc"], bt["elp"], bt["ne"], u0=bt["u0"])
+    idx = np.sort(np.random.default_rng(9).choice(B, 2048, replace=False))
+    sub = {k: (None if v is None else v[idx]) for k, v in bt.items()}
+    osub = {k: v[idx] for k, v in o.items()}
+    ref = _oracle_solve(coracle, dict(variant=variant, N=N, nc_max=n_cir, ne_max=n_elp), sub)
+    if prec:
+        both = (osub["status"] == 0) & (ref["status"] == 0)
+        assert both.mean() >= 0.75, both.mean()
+        err = np.abs(osub["foot"] - ref["foot"]).max(axis=1)
+        assert np.mean(err[both] <= 1e-3) >= 0.98, np.mean(err[both] <= 1e-3)
+        assert ((osub["status"] == 2) == (ref["status"] == 2)).mean() >= 0.97
+    elif N == 5:
+        _compare(osub, ref, min_conv=0.5, min_agree=0.95, min_status=0.9)
+    else:
+        _compare(osub, ref)
+
+
+def test_unconverged_iterates_track_oracle(gpu_lib, coracle):
+    """The reference uses the iterate as its plan whatever IPOPT's status (main_sim_mpc.py:117-121), so
+    instances that end with status 2 (infeasible) or -1 (iteration cap) are compared too: the GPU runs
+    the oracle's algorithm, and its last iterate lands near the oracle's on most such instances (their
+    trajectories are not contracting, so rounding-level differences can grow: a looser bar than the
+    converged one)."""
+    from alipmpc import scenes
+    bt = scenes.make_batch(4096, seed=0, n_cir=5)
+    s = gpu_lib.Solver(gpu_lib.default_cfg(0, nc_max=5, ne_max=0))
+    o = s.solve(bt["x0"], bt["goal"], bt["leg"], bt["cir"], bt["nc"], u0=bt["u0"])
+    ref = _oracle_solve(coracle, dict(variant=0, nc_max=5, ne_max=0), bt)
+    unc = (ref["status"] == 2) | (ref["status"] == -1)
+    assert unc.sum() >= 100
+    assert (o["status"][unc] == ref["status"][unc]).mean() >= 0.9
+    err = np.abs(o["foot"] - ref["foot"]).max(axis=1)[unc]
+    assert np.mean(err <= 1e-4 * np.maximum(1.0, np.abs(ref["foot"][unc]).max(axis=1))) >= 0.7, \
+        np.mean(err <= 1e-4)
+    assert np.isfinite(o["u"]).all()
+
+
+@pytest.mark.parametrize("variant,prec", [(1, 0), (1, 1), (0, 0)])
+def test_factorisation_failure_returns_last_iterate(gpu_lib, coracle, variant, prec):
+    """IPOPT's Error_In_Step_Computation path (status -3): a non-finite obstacle (kept because obstacle
+    selection is off) makes the KKT matrix non-finite, so the inertia correction cannot regularise it at
+    the first iteration.  The instance must stop with status -3 after 0 iterations, as the C oracle does,
+    returning the iterate from before the failing iteration bit for bit (= the max_iter = 0 output); the
+    other instances of the batch are unaffected."""
+    from alipmpc import scenes
+    bt = scenes.make_batch(4, seed=3, n_cir=4)
+    cir = bt["cir"].copy()
+    cir[1, 0, :] = [np.nan, 1.0, 0.5]
+    kw = dict(nc_max=4, ne_max=0, select_obs=0)
+    if prec:
+        kw["precision"] = gpu_lib.PREC_FP32
+    s = gpu_lib.Solver(gpu_lib.default_cfg(variant, 3, **kw))
+    o = s.solve(bt["x0"], bt["goal"], bt["leg"], cir, bt["nc"], u0=bt["u0"])
+    assert o["status"][1] == -3 and o["iters"][1] == 0
+    s0 = gpu_lib.Solver(gpu_lib.default_cfg(variant, 3, max_iter=0, **kw))
+    o0 = s0.solve(bt["x0"], bt["goal"], bt["leg"], cir, bt["nc"], u0=bt["u0"])
+    assert np.array_equal(o["u"][1], o0["u"][1]) and np.array_equal(o["foot"][1], o0["foot"][1])
+    assert np.isfinite(o["u"][1]).all()
+    ref = coracle.solve_batch(coracle.default_cfg(variant, 3, nc_max=4, ne_max=0, select_obs=0), bt["x0"],
+                              bt["goal"], bt["leg"], cir, bt["nc"], None, None, bt["u0"])
+    assert ref["status"][1] == -3 and ref["iters"][1] == 0
+    ok = np.array([0, 2, 3])
+    assert (o["status"][ok] != -3).all()
+
+
+def test_solve_horizon5_scipy_goldens(gpu_lib, golden):
+    """BASELINE cfg3 shape (N = 5, 5 circles + 5 ellipses) solutions pinned to the reference NLP:
+    SLSQP and trust-constr on the reference objective/constraints (g3_synthetic_modi_n5); to convergence
+    (max_iter 100), foothold within 1e-4 on every row both scipy methods agree on."""
+    d = golden("g3_synthetic_modi_n5")
+    good = (d["agree"] < 1e-8) & (d["viol"] < 1e-8)
+    s = gpu_lib.Solver(gpu_lib.default_cfg(0, 5, nc_max=5, ne_max=5, max_iter=100))
+    o = s.solve(d["x0"], d["goal"], d["leg"], d["cir"], d["nc"], d["elp"], d["ne"], u0=d["u0"])
+    err = np.max(np.abs(o["foot"] - d["foot_ref"]), axis=1)
+    assert good.sum() >= 30
+    assert np.all(err[good] < 1e-4), err[good].max()
+    s32 = gpu_lib.Solver(gpu_lib.default_cfg(0, 5, nc_max=5, ne_max=5, max_iter=100,
+                                             precision=gpu_lib.PREC_FP32))
+    o32 = s32.solve(d["x0"], d["goal"], d["leg"], d["cir"], d["nc"], d["elp"], d["ne"], u0=d["u0"])
+    err32 = np.max(np.abs(o32["foot"] - d["foot_ref"]), axis=1)
+    assert np.mean(err32[good] < 1e-3) >= 0.9
+
+
+def test_cfg1_sig_step_no_obstacles(gpu_lib, golden):
+    """BASELINE cfg1 (MPC_LIP_sig_step.py as-is: B = 1, N = 3, no obstacles) through the planner drop-in
+    MPCCBFSigStep.gen_control_test (warm start None -> [x0, x0, x0], the reference's own rule), one scene at
+    a time, against SLSQP / trust-constr on the reference (g3_synthetic_sig_step_nobs): foothold within
+    1e-4 at the reference's cap of 20 iterations on every row both scipy methods agree on; the batched
+    launch gives the same plans."""
+    import alipmpc.planner as pl
+    d = golden("g3_synthetic_sig_step_nobs")
+    good = np.nonzero((d["agree"] < 1e-8) & (d["viol"] < 1e-8))[0]
+    assert len(good) >= 30
+    errs, feet = [], []
+    for i in good:
+        ss = pl.MPCCBFSigStep([list(d["goal"][i])], [], [], [-0.5, 10.5])
+        xs, p0, hd, c2g = ss.gen_control_test(d["x0"][i], d["leg"][i], None)
+        errs.append(np.max(np.abs(np.ravel(p0) - d["foot_ref"][i])))
+        feet.append(np.ravel(p0))
+    assert max(errs) < 1e-4, max(errs)
+    s = gpu_lib.Solver(gpu_lib.default_cfg(1, 3, nc_max=0, ne_max=0))
+    B = len(good)
+    o = s.solve(d["x0"][good], d["goal"][good], d["leg"][good], np.zeros((B, 0, 3)), np.zeros(B, np.int32),
+                u0=d["u0"][good])
+    assert np.max(np.abs(o["foot"] - np.array(feet))) < 1e-12   # planner: p0 = W(u_1 - A x0) on the host

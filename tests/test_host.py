@@ -136,3 +136,69 @@ def test_sharding_and_gather_gloo_world2():
         p.join(timeout=120)
         assert p.exitcode == 0
     assert np.array_equal(full[:, 0], np.arange(10))
+
+
+def _bench_worker(rank, world, port, B_total, q):
+    """bench.py's step / gather loop and its quality all-reduce with a stub solver on CPU tensors."""
+    import torch
+    import torch.distributed as dist
+    import bench
+    from alipmpc import sharding
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lo, hi = sharding.shard_range(B_total, rank, world)
+    B, n = hi - lo, 15
+    out = {"u": torch.empty((B, n), dtype=torch.float64), "foot": torch.empty((B, 3), dtype=torch.float64),
+           "status": torch.empty(B, dtype=torch.int32), "iters": torch.empty(B, dtype=torch.int32)}
+    calls = []
+
+    def solve():   # stub "solver output": a function of the global instance index
+        g = torch.arange(lo, hi, dtype=torch.float64)
+        out["u"][:] = g[:, None] * 100 + torch.arange(n, dtype=torch.float64)
+        out["foot"][:] = -g[:, None]
+        out["status"][:] = (torch.arange(lo, hi) % 3).to(torch.int32) - 1
+        out["iters"][:] = torch.arange(lo, hi).to(torch.int32) + 7
+        calls.append(1)
+    step = bench.make_step(solve, out, n, B_total, rank, world)
+    elapsed, ev = bench.timed_loop(step, 1, 3, world, torch.device("cpu"))
+    full = step()
+    qc = bench.quality_counts(rank + 1, out["status"], torch.device("cpu"), world)
+    if rank == 0:
+        q.put((full.numpy().tolist(), qc, len(calls), elapsed))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("B_total", [11, 64])
+def test_bench_step_gather_loop_gloo_world2(B_total):
+    """bench.py at N = 2 ranks: every step solves the rank's contiguous shard and gathers the packed
+    outputs to rank 0 with sharding.gather_to_root (the benched collective), uneven shards padded
+    (B_total = 11 -> 6 + 5, as cfg4's total split over ranks that do not divide it); the quality counts
+    are summed over ranks."""
+    import multiprocessing as mp
+    import socket
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_bench_worker, args=(r, 2, port, B_total, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    full, qc, ncalls, elapsed = q.get(timeout=180)
+    for p in ps:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    full = np.array(full)
+    g = np.arange(B_total, dtype=float)
+    assert full.shape == (B_total, 15 + 5)
+    assert np.array_equal(full[:, :15], g[:, None] * 100 + np.arange(15))
+    assert np.array_equal(full[:, 15:18], np.repeat(-g[:, None], 3, 1))
+    assert np.array_equal(full[:, 18], g % 3 - 1)
+    assert np.array_equal(full[:, 19], g + 7)
+    assert ncalls == 1 + 3 + 1 and elapsed > 0
+    st = g % 3 - 1
+    assert qc["instances"] == B_total
+    assert qc["feasible_fraction"] == pytest.approx(3 / B_total)     # 1 + 2 over the two ranks
+    assert qc["converged_fraction"] == pytest.approx(np.isin(st, [0, 1]).mean())
+    assert qc["solved_fraction"] == pytest.approx((st == 0).mean())

@@ -152,6 +152,32 @@ def test_synthetic_scipy_solutions(golden, coracle, variant, name):
     assert np.all(err[good] < 1e-4), err[good].max()
 
 
+def test_synthetic_scipy_solutions_horizon5(golden, coracle):
+    """BASELINE cfg3 shape (N = 5, 5 circles + 5 ellipses): the C oracle lands on the KKT point SLSQP and
+    trust-constr find on the reference objective/constraints (g3_synthetic_modi_n5, tools/gen_goldens.py)."""
+    d = golden("g3_synthetic_modi_n5")
+    good = (d["agree"] < 1e-8) & (d["viol"] < 1e-8)
+    cfg = coracle.default_cfg(0, 5, nc_max=5, ne_max=5, max_iter=100)
+    r = coracle.solve_batch(cfg, d["x0"], d["goal"], d["leg"], d["cir"], d["nc"], d["elp"], d["ne"], d["u0"])
+    err = np.max(np.abs(r["foot"] - d["foot_ref"]), axis=1)
+    assert good.sum() >= 30
+    assert np.all(r["status"][good] == 0)
+    assert np.all(err[good] < 1e-6), err[good].max()
+
+
+def test_sig_step_no_obstacle_solutions(golden, coracle):
+    """BASELINE cfg1 (sig_step, N = 3, no obstacles): C oracle vs SLSQP / trust-constr on the reference."""
+    d = golden("g3_synthetic_sig_step_nobs")
+    good = (d["agree"] < 1e-8) & (d["viol"] < 1e-8)
+    B = len(d["x0"])
+    cfg = coracle.default_cfg(1, 3, nc_max=0, ne_max=0, max_iter=100)
+    r = coracle.solve_batch(cfg, d["x0"], d["goal"], d["leg"], np.zeros((B, 0, 3)), np.zeros(B, np.int32),
+                            None, None, d["u0"])
+    err = np.max(np.abs(r["foot"] - d["foot_ref"]), axis=1)
+    assert good.sum() >= 30
+    assert np.all(err[good] < 1e-6), err[good].max()
+
+
 def test_numpy_and_c_oracles_agree(golden, coracle):
     d = golden("g3_sup_learn")
     idx = np.arange(0, 640, 16)

@@ -531,6 +531,126 @@ def gen_g3_synthetic_dd(dd, rand_obs, n_cases):
     print(f"g3 synthetic dd: {n_cases} scenes, both scipy methods agree <1e-8 on {kept}")
 
 
+def _oracle_derivs(P, N):
+    """Analytic gradient / Jacobian of the reference LIP_Prob at horizon N (the reference's own
+    gradient/jacobian are N=3-only).  Built from what solveMPCCBF handed to cyipopt (selected obstacles,
+    goal after the detour, x0) by the numpy restatement, whose derivatives the CPU suite pins to central
+    finite differences of the reference objective/constraints (tests/test_oracle.py)."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "oracle"))
+    import np_oracle as O
+    po = P.problem_obj
+    cfg = O.default_cfg(O.VARIANT_MODI, N, select_obs=0, detour=0, nc_max=12, ne_max=12)
+    cir = np.asarray(po.cir_modi_pram, float).reshape(-1, 3)
+    elp = np.asarray(po.elp_modi_pram, float).reshape(-1, 5)
+    prob = O.Problem(cfg, np.ravel(po.xk), np.ravel(po.goal), 1, cir, elp)
+    return prob.gradient, prob.jacobian
+
+
+def _sample_scene_bounded(rand_obs, seed, num, typ, seconds=2):
+    """sample_scene, or None when rand_obs' rejection loop does not finish within `seconds`."""
+    import signal
+
+    def _raise(*_):
+        raise TimeoutError
+
+    old = signal.signal(signal.SIGALRM, _raise)
+    signal.alarm(seconds)
+    try:
+        return sample_scene(rand_obs, seed, num, typ)
+    except TimeoutError:
+        return None
+    finally:
+        signal.alarm(0)
+        signal.signal(signal.SIGALRM, old)
+
+
+def gen_g3_synthetic_modi_n5(modi, rand_obs, n_cases):
+    """BASELINE cfg3 shape (N = 5, 5 circles + 5 ellipses): scenes solved by SLSQP and trust-constr on the
+    reference objective/constraints (MPC_LIP_modi.py:430-500, which loop over N) built by the reference's
+    own MPCCBF(step=5) set-up (select_obs, cl/cu, detour goal); derivatives from _oracle_derivs."""
+    rng = np.random.default_rng(780)
+    margin = [-0.5, 10.5]
+    N = 5
+    R = {k: [] for k in ["x0", "leg", "goal", "cir", "nc", "elp", "ne", "u0", "u_ref", "foot_ref", "agree",
+                         "viol"]}
+    kept = 0
+    t = -1
+    while len(R["x0"]) < n_cases:
+        t += 1
+        scene = _sample_scene_bounded(rand_obs, 5000 + t, 10, "mix")
+        if scene is None:      # rejection sampling of 10 separated circles can fail to terminate
+            continue
+        cir, elp = scene
+        cs, es = inflate(cir, elp)
+        x0, leg = sample_state(rng, cs, es)
+        goal = [[10.0, 10.0]]
+        u0 = np.tile(x0, N)
+        res = []
+        for fn in (solve_slsqp, solve_trust):
+            def run(P, fn=fn):
+                g, J = _oracle_derivs(P, N)
+                po = P.problem_obj
+
+                class _Prob:   # reference f and c, analytic derivatives at any N
+                    objective = staticmethod(po.objective)
+                    constraints = staticmethod(po.constraints)
+                    gradient = staticmethod(g)
+                    jacobian = staticmethod(J)
+                return fn(_Prob, P.u0, P.cl, P.cu)
+            _StubProblem.solver = _wrap_solver(run)
+            mpc = modi.MPCCBF(goal, cir, cs, elp, es, margin, step=N)
+            out = mpc.gen_control_test(x0, leg, u0)
+            P = _StubProblem.last
+            u = _last_solution[0].copy()
+            c = np.asarray(P.problem_obj.constraints(u), float)
+            res.append((u, np.ravel(out[1]), violation(c, P.cl, P.cu)))
+        _StubProblem.solver = None
+        (ua, pa, va), (ub_, pb, vb) = res
+        agree = float(np.max(np.abs(pa - pb)))
+        R["x0"].append(x0); R["leg"].append(leg); R["goal"].append(np.array([10.0, 10.0]))
+        R["cir"].append(_pad(cs, 5, 3)); R["nc"].append(len(cs))
+        R["elp"].append(_pad(es, 5, 5)); R["ne"].append(len(es))
+        R["u0"].append(u0); R["u_ref"].append(ua); R["foot_ref"].append(pa)
+        R["agree"].append(agree); R["viol"].append(max(va, vb))
+        if agree < 1e-8 and max(va, vb) < 1e-8:
+            kept += 1
+    np.savez_compressed(os.path.join(OUT, "g3_synthetic_modi_n5.npz"), **{k: np.asarray(v) for k, v in R.items()})
+    print(f"g3 synthetic modi N=5: {n_cases} scenes, both scipy methods agree <1e-8 on {kept}")
+
+
+def gen_g3_sig_step_nobs(sig, n_cases):
+    """BASELINE cfg1 (MPC_LIP_sig_step.py, N = 3, no obstacles): the reference set-up and callbacks
+    (MPC_LIP_sig_step.py:184-278, 372-496), solved by SLSQP and trust-constr; warm start None ->
+    [x0, x0, x0] as the reference does (:186-187)."""
+    rng = np.random.default_rng(781)
+    margin = [-0.5, 10.5]
+    R = {k: [] for k in ["x0", "leg", "goal", "u0", "u_ref", "foot_ref", "agree", "viol"]}
+    kept = 0
+    for t in range(n_cases):
+        x0, leg = sample_state(rng, np.zeros((0, 3)), np.zeros((0, 5)))
+        goal = [[10.0, 10.0]] if t % 4 else [list(rng.uniform(3.0, 10.0, 2))]
+        res = []
+        for fn in (solve_slsqp, solve_trust):
+            _StubProblem.solver = _wrap_solver(lambda P, fn=fn: fn(P.problem_obj, P.u0, P.cl, P.cu))
+            mpc = sig.MPCCBF(goal, [], [], margin)
+            out = mpc.gen_control_test(x0, leg, None)
+            P = _StubProblem.last
+            u = _last_solution[0].copy()
+            c = np.asarray(P.problem_obj.constraints(u), float)
+            res.append((u, np.ravel(out[1]), violation(c, P.cl, P.cu)))
+        _StubProblem.solver = None
+        (ua, pa, va), (ub_, pb, vb) = res
+        agree = float(np.max(np.abs(pa - pb)))
+        R["x0"].append(x0); R["leg"].append(leg); R["goal"].append(np.ravel(goal))
+        R["u0"].append(np.tile(x0, 3)); R["u_ref"].append(ua); R["foot_ref"].append(pa)
+        R["agree"].append(agree); R["viol"].append(max(va, vb))
+        if agree < 1e-8 and max(va, vb) < 1e-8:
+            kept += 1
+    np.savez_compressed(os.path.join(OUT, "g3_synthetic_sig_step_nobs.npz"),
+                        **{k: np.asarray(v) for k, v in R.items()})
+    print(f"g3 synthetic sig_step, no obstacles: {n_cases} scenes, both scipy methods agree <1e-8 on {kept}")
+
+
 # ----------------------------------------------------------------------------------------------
 def gen_g4(modi, sig):
     rng = np.random.default_rng(99)
@@ -640,6 +760,10 @@ def main():
         gen_g3_synthetic(modi, sig, rand_obs, 16 if a.quick else 48, "sig_step")
     if not only or "g3dd" in only:
         gen_g3_synthetic_dd(dd, rand_obs, 16 if a.quick else 48)
+    if not only or "g3n5" in only:
+        gen_g3_synthetic_modi_n5(modi, rand_obs, 12 if a.quick else 128)
+    if not only or "g3nobs" in only:
+        gen_g3_sig_step_nobs(sig, 12 if a.quick else 48)
     return 0
 
 

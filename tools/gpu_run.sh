@@ -1,0 +1,41 @@
+#!/bin/bash
+# GPU-box driver for one iteration: `tools/gpu_run.sh TAG [tests] [bench] [configs] [prof]`.
+# Every GPU step has its own time limit; the chain stops at the first failure.
+set -u
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/$1
+shift
+mkdir -p $OUT
+export TMPDIR=/tmp
+for what in "$@"; do
+  case $what in
+  tests)
+    echo "=== pytest -m gpu"
+    timeout -k 10 900 python -u -m pytest $R/tests -x -v --timeout 120 --timeout-method thread -m gpu > $OUT/pytest_gpu.log 2>&1; rc=$?
+    tail -4 $OUT/pytest_gpu.log; [ $rc -eq 0 ] || { grep -B5 -A40 "FAILED\|Error" $OUT/pytest_gpu.log | head -80; exit $rc; }
+    echo "=== smoke"
+    timeout -k 10 300 python -c "import sys; sys.path.insert(0,'$R'); import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { cat $OUT/smoke.log; exit 1; }
+    cat $OUT/smoke.log ;;
+  bench)
+    echo "=== bench (default = cfg2)"
+    timeout -k 10 300 python $R/bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; }
+    cat $OUT/bench.json ;;
+  configs)
+    for c in cfg3 cfg4 cfg5 cfg1; do
+      echo "=== bench $c"
+      timeout -k 10 300 python $R/bench.py --config $c --steps 5 --no-cpu-baseline --sweep-batch 0 > $OUT/bench_$c.json 2> $OUT/bench_$c.err || { tail -20 $OUT/bench_$c.err; exit 1; }
+      python -c "import json;d=json.load(open('$OUT/bench_$c.json'));print('$c', round(d['value']), d['ms_per_step'], d['config']['mean_iters'], d.get('feasible'))"
+    done ;;
+  prof)
+    cd /tmp
+    echo "=== rocprofv3 kernel trace"
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_kt -o kt -- python3 $R/bench.py --steps 10 --no-cpu-baseline > $OUT/prof_kt.log 2>&1 || { tail -20 $OUT/prof_kt.log; exit 1; }
+    for pmc in FETCH_SIZE WRITE_SIZE "SQ_INSTS SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES" "SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
+      tag=$(echo $pmc | cut -d' ' -f1)
+      echo "=== rocprofv3 --pmc $pmc"
+      timeout -s KILL 120 rocprofv3 --pmc $pmc --output-format csv -d $OUT/pmc_$tag -o pmc -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --sweep-batch 0 > $OUT/pmc_$tag.log 2>&1 || { tail -20 $OUT/pmc_$tag.log; exit 1; }
+    done
+    cd $R ;;
+  esac
+done
+echo "=== done"
