@@ -78,6 +78,10 @@ extern "C" {
 #define ALIPMPC_EHIP (-3)
 #define ALIPMPC_EUNSUPPORTED (-4)
 
+/* cfg.program */
+#define ALIPMPC_PROGRAM_WAVE 0
+#define ALIPMPC_PROGRAM_LANE 1
+
 /* hip_stream value meaning "device pointers, asynchronous on the null (default) stream" */
 #define ALIPMPC_STREAM_NULL ((void*)(intptr_t)-1)
 
@@ -108,6 +112,12 @@ typedef struct alipmpc_cfg {
     double detect_r2;   /* select_obs range^2 */
     double dd_t;        /* DD control-smoothness weight */
     double mu_init;     /* initial barrier parameter */
+    int32_t program;    /* device program (no reference counterpart; the arithmetic of the interior point is the
+                           same in both): ALIPMPC_PROGRAM_WAVE — one instance per wavefront (solve_kernel,
+                           latency-optimised: small batches); ALIPMPC_PROGRAM_LANE — one instance per lane
+                           (lane_kernel, throughput-optimised: batches of 10^5+ instances; N = 3 with circles only,
+                           modi / sig_step, otherwise alipmpc_create returns ALIPMPC_EUNSUPPORTED).  A per-handle
+                           choice, never a function of B: an instance's result does not depend on its batch. */
 } alipmpc_cfg;
 
 /* Fill *out with the reference's constants for a variant and horizon.  nc_max = ne_max = 6, precision
@@ -204,13 +214,18 @@ int32_t alipmpc_trace_len(const alipmpc_cfg* cfg);
 int alipmpc_trace_batch(void* handle, int64_t B, const double* x0, const double* u, double* trace,
                         void* hip_stream);
 
-/* Instances this handle's solve kernel holds resident on its device at once (resident workgroups x 4
- * waves, one instance per wave).  Every LIP solve / rollout launch is a persistent grid of at most the
+/* Instances this handle's solve kernel holds resident on its device at once (solve_kernel: resident
+ * workgroups x 4 waves, one instance per wave; lane_kernel: resident waves x instances per wave).  Every LIP solve / rollout launch is a persistent grid of at most the
  * resident workgroups whose waves pull instances from a per-launch work queue (a wave that finishes a
  * short solve takes the next instance), so one program solves every batch size and an instance's result
  * does not depend on B (a batch solved whole or in chunks is bit-identical).  0 for the DD variant
  * (always one wave per instance).  No reference counterpart (scheduling of the batched replacement). */
 int alipmpc_solve_slots(void* handle, int64_t* slots);
+
+/* The device program this handle's solves run (cfg.program): "solve_kernel<N,rows/4,type>" (one instance per
+ * wavefront), "lane_kernel<N,circle slots,modi,type>" (one instance per lane) or "dd_solve_kernel<N,row
+ * groups>".  No reference counterpart.  The string is owned by the library. */
+const char* alipmpc_solve_program(void* handle);
 
 /* Duration in milliseconds of the most recent solve kernel launch on this handle, measured with HIP
  * events on the launch stream (0 if none). */

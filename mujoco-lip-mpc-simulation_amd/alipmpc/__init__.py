@@ -5,9 +5,11 @@
   planner      MPCCBF drop-in (reference MPC_LIP_modi.MPCCBF signatures) + solve_batch
 """
 from ._lib import (Cfg, Solver, default_cfg, load, lib_path, num_vars, rows_per_step, trace_len, EXPORTS, STATUS_NAMES,
-                   VARIANT_MODI, VARIANT_SIG_STEP, VARIANT_DD, PREC_FP64, PREC_FP32, ROLLOUT_DONE, FP32_TOL,
+                   VARIANT_MODI, VARIANT_SIG_STEP, VARIANT_DD, PREC_FP64, PREC_FP32, PROGRAM_WAVE, PROGRAM_LANE,
+                   ROLLOUT_DONE, FP32_TOL,
                    FP32_ACCEPTABLE_TOL, FP32_TOL_LONG, FP32_ACCEPTABLE_TOL_LONG)
 
 __all__ = ["Cfg", "Solver", "default_cfg", "load", "lib_path", "num_vars", "rows_per_step", "trace_len", "EXPORTS",
-           "STATUS_NAMES", "VARIANT_MODI", "VARIANT_SIG_STEP", "VARIANT_DD", "PREC_FP64", "PREC_FP32", "ROLLOUT_DONE", "FP32_TOL", "FP32_ACCEPTABLE_TOL",
+           "STATUS_NAMES", "VARIANT_MODI", "VARIANT_SIG_STEP", "VARIANT_DD", "PREC_FP64", "PREC_FP32",
+           "PROGRAM_WAVE", "PROGRAM_LANE", "ROLLOUT_DONE", "FP32_TOL", "FP32_ACCEPTABLE_TOL",
            "FP32_TOL_LONG", "FP32_ACCEPTABLE_TOL_LONG"]

@@ -14,6 +14,7 @@ from . import build as _build
 
 VARIANT_MODI, VARIANT_SIG_STEP, VARIANT_DD = 0, 1, 2
 PREC_FP64, PREC_FP32 = 0, 1
+PROGRAM_WAVE, PROGRAM_LANE = 0, 1   # cfg.program: one instance per wavefront / per lane (include/alipmpc.h)
 
 STATUS_NAMES = {0: "Solve_Succeeded", 1: "Solved_To_Acceptable_Level", 2: "Infeasible_Problem_Detected",
                 -1: "Maximum_Iterations_Exceeded", -3: "Error_In_Step_Computation",
@@ -29,7 +30,8 @@ class Cfg(ctypes.Structure):
                 ("N", "nc_max", "ne_max", "variant", "max_iter", "precision", "select_obs", "detour")] + \
                [(k, ctypes.c_double) for k in
                 ("tol", "acceptable_tol", "dt", "H", "g", "leg2_max", "bvx_lo", "bvx_hi", "bvy_lo", "bvy_hi",
-                 "dtheta_max", "q", "p", "r", "gamma", "s", "detect_r2", "dd_t", "mu_init")]
+                 "dtheta_max", "q", "p", "r", "gamma", "s", "detect_r2", "dd_t", "mu_init")] + \
+               [("program", ctypes.c_int32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -37,8 +39,8 @@ class Cfg(ctypes.Structure):
 
 EXPORTS = ("alipmpc_default_cfg", "alipmpc_rows_per_step", "alipmpc_num_vars", "alipmpc_create",
            "alipmpc_solve_batch", "alipmpc_eval_batch", "alipmpc_rollout_batch", "alipmpc_trace_len",
-           "alipmpc_trace_batch", "alipmpc_solve_slots", "alipmpc_last_kernel_ms", "alipmpc_last_error",
-           "alipmpc_destroy")
+           "alipmpc_trace_batch", "alipmpc_solve_slots", "alipmpc_solve_program", "alipmpc_last_kernel_ms",
+           "alipmpc_last_error", "alipmpc_destroy")
 
 _lib = None
 
@@ -82,6 +84,9 @@ def load(build_if_missing=True):
     if hasattr(L, "alipmpc_solve_slots"):     # (absent from older dev builds used for A/B timing)
         L.alipmpc_solve_slots.argtypes = [P, ctypes.POINTER(ctypes.c_int64)]
         L.alipmpc_solve_slots.restype = ctypes.c_int
+    if hasattr(L, "alipmpc_solve_program"):
+        L.alipmpc_solve_program.argtypes = [P]
+        L.alipmpc_solve_program.restype = ctypes.c_char_p
     L.alipmpc_last_kernel_ms.argtypes = [P]
     L.alipmpc_last_kernel_ms.restype = ctypes.c_double
     L.alipmpc_last_error.argtypes = [P]
@@ -183,6 +188,10 @@ class Solver:
 
     def last_kernel_ms(self):
         return float(self._L.alipmpc_last_kernel_ms(self._h))
+
+    def solve_program(self):
+        """The device program this handle's solves run (include/alipmpc.h: alipmpc_solve_program)."""
+        return self._L.alipmpc_solve_program(self._h).decode()
 
     def solve_slots(self):
         """Instances the solve kernel holds resident at once; larger batches run the persistent

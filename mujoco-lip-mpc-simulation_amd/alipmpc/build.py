@@ -2,9 +2,9 @@
 
 The library is the product: there is no CPU execution path behind it.
 
-csrc/alipmpc.hip is compiled as 7 translation units in parallel — ALIP_PART=0 (host code, C ABI, rollout
-kernels) and ALIP_PART=1..6 (the solve/eval kernels of one horizon N each, fp64 and fp32) — and linked into
-one shared library.  `ALIPMPC_SINGLE_TU=1` builds it as one TU instead (slower, same code).
+csrc/alipmpc.hip is compiled as 9 translation units in parallel — ALIP_PART=0 (host code, C ABI, rollout
+kernels), ALIP_PART=1..6 (the solve/eval kernels of one horizon N each, fp64 and fp32) and ALIP_PART=7/8 (the
+lane solver of csrc/lane_solve.inc, fp64 / fp32) — and linked into one shared library.  `ALIPMPC_SINGLE_TU=1` builds it as one TU instead (slower, same code).
 """
 import os
 import subprocess
@@ -16,9 +16,10 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)                         # mujoco-lip-mpc-simulation_amd/
 REPO = os.path.dirname(ROOT)
 SRC = os.path.join(ROOT, "csrc", "alipmpc.hip")
+INC = os.path.join(ROOT, "csrc", "lane_solve.inc")
 HDR = os.path.join(REPO, "include", "alipmpc.h")
 LIB = os.path.join(PKG, "libalipmpc.so")
-PARTS = range(0, 7)
+PARTS = range(0, 9)
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = ["--offload-arch=gfx950"]
@@ -33,7 +34,7 @@ def needs_build():
     if not os.path.exists(LIB):
         return True
     t = os.path.getmtime(LIB)
-    return any(os.path.getmtime(p) > t for p in (SRC, HDR, __file__))
+    return any(os.path.getmtime(p) > t for p in (SRC, INC, HDR, __file__))
 
 
 def _run(cmd, verbose):

@@ -33,6 +33,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <type_traits>
 #include <unordered_map>
 #include <vector>
 
@@ -46,6 +47,7 @@
 #define ALIP_PART_HOST (ALIP_PART == 0)
 #define ALIP_PART_N(k) (ALIP_PART == (k))
 #endif
+// ALIP_PART 7 / 8: the lane solver's fp64 / fp32 kernels (lane_solve.inc)
 
 namespace alip {
 
@@ -94,6 +96,9 @@ struct KP {
     double* cu_out;
     double* goal_eff_out;
     int8_t* active_out;
+    // lane-solver constants (lane_solve.inc, LK_* slots) in device memory, fp64 and an fp32 copy
+    const double* lkd;
+    const float* lkfd;
 };
 
 constexpr int KP_DOUBLES = (int)((sizeof(KP) + 15) / 16 * 2);
@@ -1948,6 +1953,8 @@ __global__ __launch_bounds__(256, (solve_waves<KSM, R>())) void solve_kernel(KP 
     queue_exit(q);
 }
 
+#include "lane_solve.inc"
+
 // ------------------------------------------------------------------------------------------------
 // eval kernel ("Jacobian sweep"): f, grad f, c, J, cl, cu, goal_eff, row_active at given u
 // ------------------------------------------------------------------------------------------------
@@ -3170,7 +3177,7 @@ static void set_smem(const void* f, size_t smem)
 }
 
 // workgroups of kernel f resident on the whole device at once (occupancy x CUs), cached per (f, smem)
-static unsigned resident_blocks(const void* f, size_t smem)
+static unsigned resident_blocks(const void* f, size_t smem, int threads = WAVE * WAVES_PER_BLOCK)
 {
     static std::mutex mtx;
     static std::map<std::pair<const void*, size_t>, unsigned> cache[64];
@@ -3182,7 +3189,7 @@ static unsigned resident_blocks(const void* f, size_t smem)
     if (it != c.end()) return it->second;
     int per_cu = 0, cus = 0;
     unsigned r = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, WAVE * WAVES_PER_BLOCK, smem) == hipSuccess &&
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, threads, smem) == hipSuccess &&
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && per_cu > 0 && cus > 0)
         r = (unsigned)per_cu * (unsigned)cus;
     c[{f, smem}] = r;
@@ -3292,6 +3299,53 @@ ALIP_LAUNCHERS(5)
 ALIP_LAUNCHERS(6)
 #endif
 
+// lane solver (lane_solve.inc): N = 3, circles only, NC = compiled circle slots (>= cfg.nc_max).  A persistent
+// grid of at most the resident one-wave workgroups; each lane takes instances from the launch's work queue.
+template <int N, int NC, bool MODI, class R>
+void launch_lane_t(const KP& P, hipStream_t st, unsigned* res_out)
+{
+    auto kern = lane_kernel<N, NC, MODI, R>;
+    const unsigned res = resident_blocks((const void*)kern, 0, WAVE);
+    if (res_out) {
+        *res_out = res;
+        return;
+    }
+    const unsigned need = (unsigned)((P.B + WAVE - 1) / WAVE);
+    // small batches are spread over every resident wave (the kernel's first fetch takes ceil(B / grid))
+    const unsigned grid = res > 0 ? res : (need > 0 ? need : 1u);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(WAVE), 0, st, P);
+}
+template <class R>
+hipError_t launch_lane_r(int nct, bool modi, const KP& P, hipStream_t st, unsigned* res_out)
+{
+    if (modi) {
+        if (nct == 0) launch_lane_t<3, 0, true, R>(P, st, res_out);
+        else if (nct == 5) launch_lane_t<3, 5, true, R>(P, st, res_out);
+        else if (nct == 6) launch_lane_t<3, 6, true, R>(P, st, res_out);
+        else return hipErrorInvalidValue;
+    } else {
+        if (nct == 0) launch_lane_t<3, 0, false, R>(P, st, res_out);
+        else if (nct == 5) launch_lane_t<3, 5, false, R>(P, st, res_out);
+        else if (nct == 6) launch_lane_t<3, 6, false, R>(P, st, res_out);
+        else return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+hipError_t launch_lane_f64(int nct, bool modi, const KP& P, hipStream_t st, unsigned* res_out);
+hipError_t launch_lane_f32(int nct, bool modi, const KP& P, hipStream_t st, unsigned* res_out);
+#if !defined(ALIP_PART) || ALIP_PART == 7
+hipError_t launch_lane_f64(int nct, bool modi, const KP& P, hipStream_t st, unsigned* res_out)
+{
+    return launch_lane_r<double>(nct, modi, P, st, res_out);
+}
+#endif
+#if !defined(ALIP_PART) || ALIP_PART == 8
+hipError_t launch_lane_f32(int nct, bool modi, const KP& P, hipStream_t st, unsigned* res_out)
+{
+    return launch_lane_r<float>(nct, modi, P, st, res_out);
+}
+#endif
+
 }  // namespace alip
 
 #if ALIP_PART_HOST
@@ -3311,6 +3365,11 @@ struct Handle {
     double* dEp = nullptr;
     double* dGu = nullptr;
     double* dEu = nullptr;
+    // lane solver (lane_solve.inc): constants and the compiled circle-slot count it runs with (-1: the
+    // per-wave solve_kernel serves this configuration)
+    double* dlk = nullptr;
+    float* dlkf = nullptr;
+    int lane_nct = -1;
     // work-queue counter pairs of persistent solve launches (a ring: launches in flight on different
     // streams use different pairs; each pair is reset by the last wave of the launch that used it)
     static constexpr unsigned NQ = 64;
@@ -3424,6 +3483,71 @@ void build_tables(const alipmpc_cfg& cfg, int NCPP, int NCPU, std::vector<double
     (void)np_;
 }
 
+// lane-solver constants (lane::LK_* slots): the ALIP step map per axis, W, the foothold sensitivities
+// d px_k / d fx_j = (Abar^(k-1-j) bbar)[0] and d vx_k / d fx_j = (...)[1], the relaxed (IPOPT
+// bound_relax_factor 1e-8, as the oracle) and original bounds, weights and tolerances
+void lane_constants(const alipmpc_cfg& cfg, double* lk)
+{
+    using namespace alip::lane;
+    for (int i = 0; i < 48; ++i) lk[i] = 0.0;
+    const double b = std::sqrt(cfg.g / cfg.H), T = cfg.dt;
+    const double ch = std::cosh(b * T), sh = std::sinh(b * T);
+    lk[LK_CH] = ch;
+    lk[LK_SHB] = sh / b;
+    lk[LK_BSH] = sh * b;
+    lk[LK_OMC] = 1.0 - ch;
+    const double a_ = 5.0, b_ = 1.0;
+    const double Dd = a_ * (ch - 1) * (ch - 1) + b_ * (sh * b) * (sh * b);
+    lk[LK_WCH] = -a_ * (ch - 1) / Dd;
+    lk[LK_WSH] = -b_ * sh * b / Dd;
+    double v0 = 1.0 - ch, v1 = -sh * b;
+    for (int m = 0; m < 6; ++m) {
+        lk[LK_SP + m] = v0;
+        lk[LK_SV + m] = v1;
+        const double w0 = ch * v0 + (sh / b) * v1, w1 = sh * b * v0 + ch * v1;
+        v0 = w0;
+        v1 = w1;
+    }
+    auto rl = [](double x) { return x - 1e-8 * std::fmax(1.0, std::fabs(x)); };
+    auto ru = [](double x) { return x + 1e-8 * std::fmax(1.0, std::fabs(x)); };
+    lk[LK_VXL] = rl(cfg.bvx_lo);
+    lk[LK_VXU] = ru(cfg.bvx_hi);
+    lk[LK_VYLP] = rl(cfg.bvy_lo);
+    lk[LK_VYUP] = ru(cfg.bvy_hi);
+    lk[LK_VYLN] = rl(-cfg.bvy_hi);
+    lk[LK_VYUN] = ru(-cfg.bvy_lo);
+    lk[LK_CIRL] = rl(0.0);
+    lk[LK_LEGL] = rl(0.0);
+    lk[LK_LEGU] = ru(cfg.leg2_max);
+    lk[LK_DTL] = rl(-cfg.dtheta_max);
+    lk[LK_DTU] = ru(cfg.dtheta_max);
+    lk[LK_OVXL] = cfg.bvx_lo;
+    lk[LK_OVXU] = cfg.bvx_hi;
+    lk[LK_OVYLP] = cfg.bvy_lo;
+    lk[LK_OVYUP] = cfg.bvy_hi;
+    lk[LK_OVYLN] = -cfg.bvy_hi;
+    lk[LK_OVYUN] = -cfg.bvy_lo;
+    lk[LK_OLEGU] = cfg.leg2_max;
+    lk[LK_ODT] = cfg.dtheta_max;
+    lk[LK_Q] = cfg.q;
+    lk[LK_P] = cfg.p;
+    lk[LK_R] = cfg.r;
+    lk[LK_GM1] = cfg.gamma - 1.0;
+    lk[LK_S] = cfg.s;
+    lk[LK_TOL] = cfg.tol;
+    lk[LK_ACC] = cfg.acceptable_tol;
+    lk[LK_MU0] = cfg.mu_init;
+    lk[LK_DET2] = cfg.detect_r2;
+}
+
+// the compiled lane-solver instance (circle slots) serving cfg, or -1 when none does: N = 3 with circles
+// only (<= 6 slots), modi / sig_step (BASELINE cfg1/2/4/5 shapes)
+int lane_slots_for(const alipmpc_cfg& c)
+{
+    if (c.variant == ALIPMPC_VARIANT_DD || c.N != 3 || c.ne_max != 0 || c.nc_max > 6) return -1;
+    return c.nc_max == 0 ? 0 : c.nc_max <= 5 ? 5 : 6;
+}
+
 size_t smem_bytes(const Handle* h, bool solve)
 {
     if (h->cfg.variant == ALIPMPC_VARIANT_DD) {
@@ -3493,6 +3617,8 @@ KP make_kp(const Handle* h, long long B, bool solve)
     P.Gu = h->dGu;
     P.Eu = h->dEu;
     P.B = B;
+    P.lkd = h->dlk;
+    P.lkfd = h->dlkf;
     if (solve && c.variant != ALIPMPC_VARIANT_DD) P.queue = h->dq + 2 * (h->qi.fetch_add(1u) % Handle::NQ);
     return P;
 }
@@ -3526,6 +3652,9 @@ hipError_t launch(const Handle* h, bool solve, const KP& P, hipStream_t st, unsi
         }
         return hipErrorInvalidValue;
     }
+    if (solve && h->lane_nct >= 0)
+        return f32 ? launch_lane_f32(h->lane_nct, h->cfg.variant == ALIPMPC_VARIANT_MODI, P, st, res_out)
+                   : launch_lane_f64(h->lane_nct, h->cfg.variant == ALIPMPC_VARIANT_MODI, P, st, res_out);
     switch (h->N) {
     case 1: return launch_lip_1(solve, f32, P, smem, st, res_out);
     case 2: return launch_lip_2(solve, f32, P, smem, st, res_out);
@@ -3651,6 +3780,7 @@ int alipmpc_create(const alipmpc_cfg* cfg, int device, void** handle)
         cfg->nc_max + cfg->ne_max > ALIPMPC_MAX_OBS || cfg->max_iter < 0 || cfg->max_iter > FILTER_CAP - 2)
         return ALIPMPC_EINVAL;
     if (cfg->precision != ALIPMPC_PREC_FP64 && cfg->precision != ALIPMPC_PREC_FP32) return ALIPMPC_EINVAL;
+    if (cfg->program != ALIPMPC_PROGRAM_WAVE && cfg->program != ALIPMPC_PROGRAM_LANE) return ALIPMPC_EINVAL;
     // fp32 arithmetic is implemented for the LIP solve kernels (modi, sig_step)
     if (cfg->precision == ALIPMPC_PREC_FP32 && cfg->variant == ALIPMPC_VARIANT_DD) return ALIPMPC_EUNSUPPORTED;
     if (cfg->variant != ALIPMPC_VARIANT_MODI && cfg->variant != ALIPMPC_VARIANT_SIG_STEP &&
@@ -3709,11 +3839,30 @@ int alipmpc_create(const alipmpc_cfg* cfg, int device, void** handle)
     };
     if (!up(&h->dGp, Gp) || !up(&h->dEp, Ep) || !up(&h->dGu, Gu) || !up(&h->dEu, Eu) ||
         hipMalloc(&h->dq, 2 * Handle::NQ * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&h->dlk, 48 * sizeof(double)) != hipSuccess || hipMalloc(&h->dlkf, 48 * sizeof(float)) != hipSuccess ||
         hipMemset(h->dq, 0, 2 * Handle::NQ * sizeof(uint32_t)) != hipSuccess ||
         hipStreamCreateWithFlags(&h->own, hipStreamNonBlocking) != hipSuccess ||
         !create_events(h)) {
         alipmpc_destroy(h);
         return ALIPMPC_EHIP;
+    }
+    {
+        double lk[48];
+        float lkf[48];
+        lane_constants(h->cfg, lk);
+        for (int i = 0; i < 48; ++i) lkf[i] = (float)lk[i];
+        if (hipMemcpy(h->dlk, lk, sizeof(lk), hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(h->dlkf, lkf, sizeof(lkf), hipMemcpyHostToDevice) != hipSuccess) {
+            alipmpc_destroy(h);
+            return ALIPMPC_EHIP;
+        }
+        if (h->cfg.program == ALIPMPC_PROGRAM_LANE) {
+            h->lane_nct = lane_slots_for(h->cfg);
+            if (h->lane_nct < 0) {
+                alipmpc_destroy(h);
+                return ALIPMPC_EUNSUPPORTED;
+            }
+        }
     }
     if (smem_bytes(h, true) > 160 * 1024 || smem_bytes(h, false) > 160 * 1024) {
         alipmpc_destroy(h);
@@ -4102,8 +4251,30 @@ int alipmpc_solve_slots(void* handle, int64_t* slots)
     unsigned res = 0;
     KP P = make_kp(h, 1, true);
     HIPCHK(h, launch(h, true, P, h->own, &res));
-    *slots = (int64_t)res * WAVES_PER_BLOCK;
+    if (h->lane_nct >= 0)
+        *slots = (int64_t)res * (h->cfg.precision == ALIPMPC_PREC_FP32 ? lane::lanes_of<float>() : lane::lanes_of<double>());
+    else
+        *slots = (int64_t)res * WAVES_PER_BLOCK;
     return ALIPMPC_OK;
+}
+
+const char* alipmpc_solve_program(void* handle)
+{
+    Handle* h = (Handle*)handle;
+    if (!h) return "";
+    static thread_local char buf[96];
+    const alipmpc_cfg& c = h->cfg;
+    const char* r = c.precision == ALIPMPC_PREC_FP32 ? "float" : "double";
+    if (c.variant == ALIPMPC_VARIANT_DD) {
+        const int rpl = h->mo4 / WAVE;
+        std::snprintf(buf, sizeof(buf), "dd_solve_kernel<%d,%d>", h->N, rpl);
+    } else if (h->lane_nct >= 0) {
+        std::snprintf(buf, sizeof(buf), "lane_kernel<%d,%d,%s,%s>", h->N, h->lane_nct,
+                      c.variant == ALIPMPC_VARIANT_MODI ? "true" : "false", r);
+    } else {
+        std::snprintf(buf, sizeof(buf), "solve_kernel<%d,%d,%s>", h->N, h->mo4 / 4, r);
+    }
+    return buf;
 }
 
 void alipmpc_destroy(void* handle)
@@ -4115,6 +4286,8 @@ void alipmpc_destroy(void* handle)
     for (double* d : {h->dGp, h->dEp, h->dGu, h->dEu})
         if (d) (void)hipFree(d);
     if (h->dq) hipFree(h->dq);
+    if (h->dlk) hipFree(h->dlk);
+    if (h->dlkf) hipFree(h->dlkf);
     if (h->stage) hipFree(h->stage);
     if (h->rstage) hipFree(h->rstage);
     for (auto& pr : h->ev)
