@@ -35,14 +35,20 @@ sys.path.insert(0, os.path.join(ROOT, "mujoco-lip-mpc-simulation_amd"))
 FP64_PEAK_TFLOPS = 78.6      # MI355X FP64 matrix / vector peak (AMD spec; MI355X_MICROARCH.md lists no FP64 row)
 FP32_PEAK_TFLOPS = 157.3     # MI355X FP32 matrix = vector peak (MI355X_MICROARCH.md)
 
-# BASELINE.json configs: (instances, per_gpu?, horizon, circles, ellipses, precision, distinct fields)
+# BASELINE.json configs: (instances, per_gpu?, horizon, circles, ellipses, precision, distinct fields).
+# program: the device program (cfg.program, include/alipmpc.h) — "wave" (one instance per wavefront: the
+# latency-bound small batches: cfg1, cfg2, and cfg4's 32k-instance shards at 8 GPUs), "lane" (one instance
+# per lane: batches of 10^5+ instances per GPU; N = 3 circles only), "auto" = lane when the rank's shard
+# has at least LANE_MIN_B instances (the measured crossover, profiles/r2/) and the shape allows it.
 CONFIGS = {
-    "cfg1": dict(batch=1, per_gpu=True, horizon=3, circles=0, ellipses=0, fp32=False, variant="sig_step"),
-    "cfg2": dict(batch=4096, per_gpu=True, horizon=3, circles=5, ellipses=0, fp32=False),
-    "cfg3": dict(batch=65536, per_gpu=True, horizon=5, circles=5, ellipses=5, fp32=False),
-    "cfg4": dict(batch=262144, per_gpu=False, horizon=3, circles=5, ellipses=0, fp32=False),
-    "cfg5": dict(batch=1048576, per_gpu=False, horizon=3, circles=5, ellipses=0, fp32=True),
+    "cfg1": dict(batch=1, per_gpu=True, horizon=3, circles=0, ellipses=0, fp32=False, variant="sig_step",
+                 program="wave"),
+    "cfg2": dict(batch=4096, per_gpu=True, horizon=3, circles=5, ellipses=0, fp32=False, program="wave"),
+    "cfg3": dict(batch=65536, per_gpu=True, horizon=5, circles=5, ellipses=5, fp32=False, program="wave"),
+    "cfg4": dict(batch=262144, per_gpu=False, horizon=3, circles=5, ellipses=0, fp32=False, program="auto"),
+    "cfg5": dict(batch=1048576, per_gpu=False, horizon=3, circles=5, ellipses=0, fp32=True, program="auto"),
 }
+LANE_MIN_B = 65536
 HBM_PEAK_GBS = 8000.0
 
 
@@ -53,14 +59,9 @@ def flops_per_iter(n, m, N, nobs):
     return kkt + chol + nlp
 
 
-def solve_kernel_name(N, rps, modi, fp32=False, queue=False):
-    """The solve_kernel<N, KSM, R, QUEUE> instance the library dispatches (csrc/alipmpc.hip: ksm_of,
-    launch_solve): constraint rows in the solve layout (f_en split into two rows for modi) + N objective
-    rows, in 4-row J-layout steps; QUEUE = the batch exceeds the resident instance slots."""
-    m = N * (rps + (1 if modi else 0))
-    rows = ((m + 3) // 4) * 4 + 4 * ((N + 3) // 4)
-    ksm = next(k for k in (8, 10, 12, 16, 24, 32, 48) if rows <= 4 * k)
-    return f"solve_kernel<{N},{ksm},{'float' if fp32 else 'double'},{'true' if queue else 'false'}>", m
+def solve_rows(N, rps, modi):
+    """Constraint rows of the solve layout (f_en split into two rows for modi)."""
+    return N * (rps + (1 if modi else 0))
 
 
 def parse():
@@ -79,6 +80,7 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")),
                     help="threads for the all-cores CPU baseline (the GPU box allots 16)")
     ap.add_argument("--sweep-batch", type=int, default=65536, help="instances for the Jacobian-sweep roofline")
+    ap.add_argument("--program", default=None, choices=["wave", "lane", "auto"], help="default: the config's")
     return ap.parse_args()
 
 
@@ -115,6 +117,11 @@ def main():
         lo, hi = sharding.shard_range(preset["batch"], rank, world)
         B = hi - lo
     prec = {"precision": alipmpc.PREC_FP32} if fp32 else {}
+    program = args.program or preset.get("program", "wave")
+    lane_ok = N == 3 and n_elp == 0 and n_cir <= 6
+    if program == "auto":
+        program = "lane" if (lane_ok and B >= LANE_MIN_B) else "wave"
+    prec["program"] = alipmpc.PROGRAM_LANE if program == "lane" else alipmpc.PROGRAM_WAVE
     cfg = alipmpc.default_cfg(variant, N, nc_max=n_cir, ne_max=n_elp, **prec)
     solver = alipmpc.Solver(cfg, device=dev.index)
     seed = args.seed * 1000 + rank
@@ -160,10 +167,12 @@ def main():
         slots = solver.solve_slots()
     except (AttributeError, RuntimeError):
         slots = None
-    kname, m = solve_kernel_name(N, solver.rps, variant == alipmpc.VARIANT_MODI, fp32,
-                                 queue=slots is not None and B > slots)
+    kname = solver.solve_program()
+    m = solve_rows(N, solver.rps, variant == alipmpc.VARIANT_MODI)
     fpi = flops_per_iter(n, m, N, n_cir + n_elp)
-    peak = FP32_PEAK_TFLOPS if fp32 else FP64_PEAK_TFLOPS
+    # the lane program's KKT system is fp64 in both precisions; its bound is vector issue (FP64 VALU peak =
+    # the FP64 matrix peak on MI355X); the wave program's KKT GEMM runs on MFMA in the solve precision
+    peak = FP32_PEAK_TFLOPS if (fp32 and program == "wave") else FP64_PEAK_TFLOPS
     launch_flops = fpi * float(iters.sum())
     achieved = launch_flops / (kernel_ms * 1e-3) / 1e12
     traffic = None
@@ -172,7 +181,7 @@ def main():
         try:
             with open(tp) as fh:
                 tj = json.load(fh)
-            if tj.get("B") == B and tj.get("N") == N and not fp32 and not n_elp:
+            if tj.get("B") == B and tj.get("N") == N and not fp32 and not n_elp and tj.get("kernel", kname) == kname:
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -213,11 +222,13 @@ def main():
                 "mean_iters": float(iters.mean()), "max_iters": int(iters.max()),
                 "status_counts": {str(k): int(v) for k, v in zip(*np.unique(status, return_counts=True))},
                 "resident_slots": slots,
-                "launch": "persistent work queue" if (slots is not None and B > slots) else "one wave per instance",
+                "program": program,
+                "launch": ("persistent work queue, one instance per lane" if program == "lane" else
+                           "persistent work queue, one instance per wavefront"),
             },
             "roofline": {
                 "kernel": kname,
-                "bound": "mfma",
+                "bound": "mfma" if program == "wave" else "valu",
                 "achieved": achieved,
                 "peak": peak,
                 "unit": "TFLOP/s",

@@ -109,9 +109,9 @@ def make_batch(B, seed=0, n_cir=5, n_elp=0, N=3, nc_max=None, ne_max=None, scene
         leg[b] = lg
         nc[b] = min(len(cs), nc_max)
         ne[b] = min(len(es), ne_max)
-        cir[b, :nc[b]] = cs[:nc[b]]
+        cir[b, :nc[b]] = np.asarray(cs, float).reshape(-1, 3)[:nc[b]]
         if ne_max:
-            elp[b, :ne[b]] = es[:ne[b]]
+            elp[b, :ne[b]] = np.asarray(es, float).reshape(-1, 5)[:ne[b]]
     u0 = np.tile(x0, (1, N))
     goal = np.tile(np.array(GOAL), (B, 1))
     return dict(x0=x0, goal=goal, leg=leg, cir=cir, nc=nc, elp=elp if ne_max else None, ne=ne if ne_max else None,

@@ -682,3 +682,132 @@ def test_cfg1_sig_step_no_obstacles(gpu_lib, golden):
     o = s.solve(d["x0"][good], d["goal"][good], d["leg"][good], np.zeros((B, 0, 3)), np.zeros(B, np.int32),
                 u0=d["u0"][good])
     assert np.max(np.abs(o["foot"] - np.array(feet))) < 1e-12   # planner: p0 = W(u_1 - A x0) on the host
+
+
+# ---------------------------------------------------------------- lane program (cfg.program = PROGRAM_LANE)
+LANE_CASES = [  # (variant, circles, precision): cfg2/cfg4 shape fp64, sup_learn slots, sig_step, cfg5 (fp32)
+    (0, 5, 0), (0, 6, 0), (1, 4, 0), (1, 0, 0), (0, 5, 1)]
+
+
+@pytest.mark.parametrize("variant,n_cir,prec", LANE_CASES)
+def test_lane_program_vs_oracle(gpu_lib, coracle, variant, n_cir, prec):
+    """The lane program (one interior-point instance per lane, csrc/lane_solve.inc) against the C oracle on
+    a seeded batch: fp64 runs the oracle's algorithm (statuses equal on >= 99 % of the instances, footholds
+    and states within 1e-4 where both converge — SURVEY 8d's bar); fp32 with test_fp32_solve_vs_oracle's
+    bars (footholds within 1e-3 where both converge, infeasibility verdicts equal on >= 97 %)."""
+    from alipmpc import scenes
+    B = 4096
+    bt = scenes.make_batch(B, seed=800 + n_cir + 10 * variant + 100 * prec, n_cir=n_cir)
+    kw = dict(nc_max=n_cir, ne_max=0, program=gpu_lib.PROGRAM_LANE)
+    if prec:
+        kw["precision"] = gpu_lib.PREC_FP32
+    s = gpu_lib.Solver(gpu_lib.default_cfg(variant, 3, **kw))
+    assert s.solve_program().startswith("lane_kernel<3,")
+    o = s.solve(bt["x0"], bt["goal"], bt["leg"], bt["cir"], bt["nc"], u0=bt["u0"])
+    ref = _oracle_solve(coracle, dict(variant=variant, nc_max=n_cir, ne_max=0), bt)
+    assert np.isfinite(o["u"]).all()
+    if prec:
+        both = (o["status"] == 0) & (ref["status"] == 0)
+        assert both.mean() >= 0.75, both.mean()
+        err = np.abs(o["foot"] - ref["foot"]).max(axis=1)
+        assert np.mean(err[both] <= 1e-3) >= 0.98, np.mean(err[both] <= 1e-3)
+        assert ((o["status"] == 2) == (ref["status"] == 2)).mean() >= 0.97
+    else:
+        _compare(o, ref, min_conv=0.8, min_agree=0.99, min_status=0.99)
+    assert np.allclose(o["u"].reshape(-1, 3, 5), o["x_pred"], rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("prec", [0, 1])
+def test_lane_program_batch_independence(gpu_lib, prec):
+    """The lane program's result for an instance does not depend on the batch: one batch above the resident
+    lane slots and the same instances in chunks of half the slots are bit-identical; NaN-filled device
+    outputs are all written (every instance solved once) and a second launch reproduces the first (the
+    queue counters reset)."""
+    import torch
+    from alipmpc import scenes
+    kw = dict(nc_max=5, ne_max=0, program=gpu_lib.PROGRAM_LANE)
+    if prec:
+        kw["precision"] = gpu_lib.PREC_FP32
+    s = gpu_lib.Solver(gpu_lib.default_cfg(0, 3, **kw))
+    slots = s.solve_slots()
+    assert slots >= 16384 and slots % 32 == 0, slots
+    B = slots + slots // 2 + 37
+    bt = scenes.make_batch_vec(B, seed=91 + prec, n_cir=5, N=3)
+    big = s.solve(bt["x0"], bt["goal"], bt["leg"], bt["cir"], bt["nc"], u0=bt["u0"])
+    ch = slots // 2
+    parts = [s.solve(bt["x0"][i:i + ch], bt["goal"][i:i + ch], bt["leg"][i:i + ch], bt["cir"][i:i + ch],
+                     bt["nc"][i:i + ch], u0=bt["u0"][i:i + ch]) for i in range(0, B, ch)]
+    for k in big:
+        assert np.array_equal(big[k], np.concatenate([p[k] for p in parts])), k
+    dev = torch.device("cuda", 0)
+    inp = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in bt.items() if v is not None}
+    inp["leg"] = inp["leg"].to(torch.int8)
+    inp["nc"] = inp["nc"].to(torch.int32)
+    for _ in range(2):
+        out = {"u": torch.full((B, 15), float("nan"), dtype=torch.float64, device=dev),
+               "foot": torch.full((B, 3), float("nan"), dtype=torch.float64, device=dev),
+               "x_pred": torch.full((B, 3, 5), float("nan"), dtype=torch.float64, device=dev),
+               "status": torch.full((B,), -99, dtype=torch.int32, device=dev),
+               "iters": torch.full((B,), -99, dtype=torch.int32, device=dev)}
+        s.solve_device(inp, out)
+        torch.cuda.synchronize()
+        got = {k: v.cpu().numpy() for k, v in out.items()}
+        for k in got:
+            assert np.array_equal(got[k], big[k]), k
+
+
+@pytest.mark.parametrize("variant,prec", [(0, 0), (1, 0), (0, 1)])
+def test_lane_program_factorisation_failure(gpu_lib, coracle, variant, prec):
+    """Error_In_Step_Computation on the lane program: a non-finite obstacle (obstacle selection off) makes the
+    KKT matrix unfactorisable at the first iteration -> status -3 after 0 iterations with the iterate from
+    before the failing iteration (= the max_iter = 0 output, bit for bit), as the C oracle; the other lanes
+    of the wave are unaffected."""
+    from alipmpc import scenes
+    bt = scenes.make_batch(4, seed=3, n_cir=4)
+    cir = bt["cir"].copy()
+    cir[1, 0, :] = [np.nan, 1.0, 0.5]
+    kw = dict(nc_max=4, ne_max=0, select_obs=0, program=gpu_lib.PROGRAM_LANE)
+    if prec:
+        kw["precision"] = gpu_lib.PREC_FP32
+    o = gpu_lib.Solver(gpu_lib.default_cfg(variant, 3, **kw)).solve(bt["x0"], bt["goal"], bt["leg"], cir, bt["nc"],
+                                                                    u0=bt["u0"])
+    assert o["status"][1] == -3 and o["iters"][1] == 0
+    o0 = gpu_lib.Solver(gpu_lib.default_cfg(variant, 3, max_iter=0, **kw)).solve(bt["x0"], bt["goal"], bt["leg"], cir,
+                                                                                bt["nc"], u0=bt["u0"])
+    assert np.array_equal(o["u"][1], o0["u"][1]) and np.array_equal(o["foot"][1], o0["foot"][1])
+    assert np.isfinite(o["u"][1]).all()
+    assert (o["status"][[0, 2, 3]] != -3).all()
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+def test_lane_program_rollout_vs_oracle(gpu_lib, coracle, variant):
+    """Closed-loop rollouts (retired instances skipped through the lane work queue) on the lane program against
+    the oracle's closed loop, with test_rollout_matches_oracle's bars."""
+    from alipmpc import scenes
+    N, B, S = 3, 256, 6
+    bt = scenes.make_batch(B, seed=191 + variant, n_cir=5, N=N)
+    x0 = bt["x0"].copy()
+    x0[:16, 0:2] = bt["goal"][:16] - np.array([0.3, 0.2])
+    u0 = np.tile(x0, (1, N))
+    s = gpu_lib.Solver(gpu_lib.default_cfg(variant, N, nc_max=5, ne_max=0, program=gpu_lib.PROGRAM_LANE))
+    o = s.rollout(x0, bt["goal"], bt["leg"], bt["cir"], bt["nc"], u0=u0, steps=S)
+    ref = coracle.rollout_batch(coracle.default_cfg(variant, N, nc_max=5, ne_max=0), x0, bt["goal"], bt["leg"],
+                                bt["cir"], bt["nc"], None, None, u0, None, steps=S, nthreads=8)
+    same_status = (o["status"] == ref["status"]).all(1)
+    fo, fr = np.nan_to_num(o["foot"], nan=1e9), np.nan_to_num(ref["foot"], nan=1e9)
+    same_path = (np.abs(fo - fr) <= 1e-4 * np.maximum(1.0, np.abs(fr))).all((1, 2))
+    assert (same_status & same_path).mean() >= 0.85
+    assert (o["steps_to_goal"] == ref["steps_to_goal"]).mean() >= 0.9
+    for b in np.nonzero(o["steps_to_goal"] > 0)[0]:
+        assert (o["status"][b, o["steps_to_goal"][b]:] == gpu_lib.ROLLOUT_DONE).all()
+
+
+def test_lane_program_unsupported_shapes(gpu_lib):
+    """The lane program serves N = 3 with circles only (<= 6 slots): other shapes are refused at create."""
+    for kw in (dict(N=5), dict(ne_max=2), dict(nc_max=8)):
+        N = kw.pop("N", 3)
+        cfg = gpu_lib.default_cfg(0, N, **{"nc_max": 5, "ne_max": 0, **kw}, program=gpu_lib.PROGRAM_LANE)
+        with pytest.raises(RuntimeError, match="EUNSUPPORTED"):
+            gpu_lib.Solver(cfg)
+    with pytest.raises(RuntimeError, match="EUNSUPPORTED"):
+        gpu_lib.Solver(gpu_lib.default_cfg(gpu_lib.VARIANT_DD, 3, nc_max=5, ne_max=0, program=gpu_lib.PROGRAM_LANE))
