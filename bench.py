@@ -81,6 +81,8 @@ def parse():
                     help="threads for the all-cores CPU baseline (the GPU box allots 16)")
     ap.add_argument("--sweep-batch", type=int, default=65536, help="instances for the Jacobian-sweep roofline")
     ap.add_argument("--program", default=None, choices=["wave", "lane", "auto"], help="default: the config's")
+    ap.add_argument("--closed-loop-steps", type=int, default=1,
+                    help="walking steps of the per-tick closed-loop figure (f_cyc = 40 solves each; 0 = skip)")
     return ap.parse_args()
 
 
@@ -191,6 +193,8 @@ def main():
     feas = feasible_fraction(alipmpc, solver, cfg, inp, out, dev, world, dist)
 
     sweep = jacobian_sweep(alipmpc, scenes, variant, args, dev) if (rank == 0 and args.sweep_batch > 0) else None
+    cl = closed_loop_rate(solver, inp, out, args.closed_loop_steps, dev) \
+        if (rank == 0 and args.closed_loop_steps > 0) else None
 
     cpu = cpu_mt = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -241,6 +245,7 @@ def main():
             "cpu_baseline": cpu,
             "cpu_baseline_allcores": cpu_mt,
             "jacobian_sweep": sweep,
+            "closed_loop": cl,
             "feasible": feas,
         }
         print(json.dumps(line))
@@ -346,6 +351,36 @@ def jacobian_sweep(alipmpc, scenes, variant, args, dev, reps=10):
     return {"kernel": f"eval_kernel<{cfg.N}>", "bound": "hbm", "batch": Bs, "bytes_per_instance": per,
             "kernel_ms": ms, "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
             "evals_per_s": Bs / (ms * 1e-3)}
+
+
+def closed_loop_rate(solver, inp, out, steps, dev, f_cyc=40):
+    """the reference driver's receding horizon at its control rate (alipmpc_closed_loop_batch:
+    f_cyc solves per walking step, each one tick closer to touchdown, warm-started from the previous plan) on
+    this rank's episodes.  Start: the bench instances' x0 with the stance on the first foothold the timed solve
+    planned (the consistent touchdown pair).  Rate = episode-ticks solved / (HIP-event time of the whole loop
+    on the launch stream: the per-tick projection, solve and update launches)."""
+    import torch
+    B = inp["x0"].shape[0]
+    st = torch.cuda.current_stream(dev)
+    cin = {"x0": inp["x0"], "foot0": out["foot"][:, 0:2].contiguous(), "goal": inp["goal"], "leg": inp["leg"],
+           "cir": inp["cir"], "nc": inp["nc"]}
+    if "elp" in inp:
+        cin["elp"], cin["ne"] = inp["elp"], inp["ne"]
+    co = {"status": torch.empty((B, steps, f_cyc), dtype=torch.int32, device=dev),
+          "iters": torch.empty((B, steps, f_cyc), dtype=torch.int32, device=dev),
+          "steps_to_goal": torch.empty((B,), dtype=torch.int32, device=dev)}
+    solver.closed_loop_device(cin, co, steps, f_cyc=f_cyc, stream=st)
+    torch.cuda.synchronize(dev)
+    solver.closed_loop_device(cin, co, steps, f_cyc=f_cyc, stream=st)
+    torch.cuda.synchronize(dev)
+    ms = solver.last_kernel_ms()
+    status = co["status"].cpu().numpy()
+    ran = status != -10
+    ticks = int(ran.sum())
+    return {"episodes": B, "steps": steps, "f_cyc": f_cyc, "ticks": ticks, "ms": ms,
+            "solves_per_s": ticks / (ms * 1e-3), "mean_iters": float(co["iters"].cpu().numpy()[ran].mean()),
+            "status_counts": {str(k): int(v) for k, v in zip(*np.unique(status[ran], return_counts=True))},
+            "program": solver.solve_program()}
 
 
 def feasible_fraction(alipmpc, solver, cfg, inp, out, dev, world, dist, chunk=65536):

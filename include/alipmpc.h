@@ -198,6 +198,38 @@ int alipmpc_rollout_batch(void* handle, int64_t B, int32_t S,
                           double* foot_traj, double* x_traj, int32_t* status_traj, int32_t* iters_traj,
                           int32_t* steps_to_goal, double* u_traj, void* hip_stream);
 
+/*
+ * Closed loop at the reference's control rate: B episodes of up to S walking steps with f_cyc MPC solves per
+ * step (main_sim_mpc.py:41,65-135, f_cyc = 40: one solve per 10 ms tick of a 0.4 s step) on an ALIP plant —
+ * the batch harness of Logger.set_stf_head / gen_nex_foot_input (data_procs/logger_mpc.py:270-371).
+ * Tick i of step s (rest_t = T - i T / f_cyc, main_sim_mpc.py:78):
+ *   i == 0: set_stf_head with the plant heading: nex_turn <- tube_func(nex_turn, hd), hd_input_pr <- avg_hd(hd),
+ *           hd_input_cos <- hd (logger_mpc.py:208-215, 270-300; nex_turn = 0 and mpc_hds_list = the initial heading
+ *           initially — the Logger's 0 in its robot frame, whose origin is the initial pose, logger_mpc.py:27,90);
+ *   x_nex = get_next_states(pos, vel, hd, [stance foot, hd_input_pr], rest_t) (MPC_LIP_modi.py:149-178);
+ *   solve at x_nex with od_ev = -leg_ind; warm start [x_nex] x 3 on the episode's first solve, then the
+ *   previous plan x_mpc_tar (logger_mpc.py:327-333 with the driver's num_step >= 1; sig_step: [g2..gN, gN]);
+ *   nex_turn <- p_list[0][2], mpc_hds_list <- hd_list;
+ *   the plant moves dt = T / f_cyc around the stance foot with the heading advancing hd_input_pr dt / T (the
+ *   model get_next_states assumes), plus a velocity kick kick * U(-1, 1) per axis from splitmix64(seed,
+ *   episode, step, tick, axis) (plant mismatch; kick = 0: the ideal plant);
+ *   after the last tick: touchdown — the stance foot becomes p_list[0][0:2] of that solve, leg_ind <- -leg_ind;
+ *   the episode stops there if any earlier solve reported close_2_goal (the driver checks real_close at the
+ *   foot change before updating it, main_sim_mpc.py:106-135).
+ * Inputs: x0 B x 5 plant state at the first touchdown, foot0 B x 2 its stance foot, goal B x 2, leg B leg_ind
+ * (the reference starts at -1), obstacles as alipmpc_solve_batch.  Outputs (any may be NULL):
+ *   foot_traj B x S x 3 (p_list[0] of each step's last solve, NaN after the stop), x_traj B x (S+1) x 5
+ *   (touchdown states), hd_traj B x S x 2 (hd_input_pr, hd_input_cos of each step), status_traj / iters_traj
+ *   B x S x f_cyc (ALIPMPC_ROLLOUT_DONE after the stop), steps_to_goal B (-1: not within S).
+ * LIP variants only (DD: ALIPMPC_EUNSUPPORTED).  Host / device pointers as alipmpc_solve_batch; S * f_cyc solve
+ * launches plus two small kernels per tick on the stream.
+ */
+int alipmpc_closed_loop_batch(void* handle, int64_t B, int32_t S, int32_t f_cyc, double kick, uint64_t seed,
+                              const double* x0, const double* foot0, const double* goal, const int8_t* leg,
+                              const double* cir, const int32_t* nc, const double* elp, const int32_t* ne,
+                              double* foot_traj, double* x_traj, double* hd_traj, int32_t* status_traj,
+                              int32_t* iters_traj, int32_t* steps_to_goal, void* hip_stream);
+
 /* Rows per planned step of alipmpc_trace_batch: 1 + len(np.arange(0, dt + 0.01, 0.01)) (42 at dt = 0.4);
  * 0 for the DD variant. */
 int32_t alipmpc_trace_len(const alipmpc_cfg* cfg);

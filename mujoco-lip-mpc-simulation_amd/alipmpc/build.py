@@ -17,6 +17,7 @@ ROOT = os.path.dirname(PKG)                         # mujoco-lip-mpc-simulation_
 REPO = os.path.dirname(ROOT)
 SRC = os.path.join(ROOT, "csrc", "alipmpc.hip")
 INC = os.path.join(ROOT, "csrc", "lane_solve.inc")
+MATH = os.path.join(ROOT, "csrc", "fastmath.inc")
 HDR = os.path.join(REPO, "include", "alipmpc.h")
 LIB = os.path.join(PKG, "libalipmpc.so")
 PARTS = range(0, 9)
@@ -34,7 +35,7 @@ def needs_build():
     if not os.path.exists(LIB):
         return True
     t = os.path.getmtime(LIB)
-    return any(os.path.getmtime(p) > t for p in (SRC, INC, HDR, __file__))
+    return any(os.path.getmtime(p) > t for p in (SRC, INC, MATH, HDR, __file__))
 
 
 def _run(cmd, verbose):

@@ -282,8 +282,6 @@ __device__ __forceinline__ T gsum(T v)
 }
 
 // ---- type-generic scalar pieces of the solve kernel (R = double | float)
-__device__ __forceinline__ void msincos(double x, double* s, double* c) { sincos(x, s, c); }
-__device__ __forceinline__ void msincos(float x, float* s, float* c) { sincosf(x, s, c); }
 
 // 4 consecutive LDS values (16-byte aligned) as b128 accesses
 __device__ __forceinline__ void ld4(const double* p, double& a, double& b, double& c, double& d)
@@ -800,6 +798,8 @@ __device__ __forceinline__ float rcp_nr(float x)
     return fmaf(y, fmaf(-x, y, 1.0f), y);
 }
 
+#include "fastmath.inc"
+
 // ------------------------------------------------------------------------------------------------
 // register Cholesky: lane i (< n) holds row i of the (regularised) KKT matrix in a[0..n-1].
 // Right-looking; column j is broadcast with readlane (uniform lane index, compile-time register).
@@ -1001,8 +1001,8 @@ template <class R>
 __device__ __forceinline__ void row_trans(int type, const R (&v)[4], R gxg, R gyg, R& a0, R& a1)
 {
     R s_, c_;
-    msincos(v[2], &s_, &c_);
-    const R at = atan2(gyg - v[1], gxg - v[0]);
+    lsincos(v[2], &s_, &c_);
+    const R at = latan2(gyg - v[1], gxg - v[0]);
     a0 = type == R_OBJ ? v[2] - at : s_;
     a1 = c_;
 }
@@ -1314,7 +1314,7 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
         const R dl = sr[q] - cl[q], du = cu[q] - sr[q];
         idl[q] = HL(q) ? R(1.0) / dl : R(0.0);
         idu[q] = HU(q) ? R(1.0) / du : R(0.0);
-        lg0 += HL(q) ? (HU(q) ? log(dl * du) : log(dl)) : (HU(q) ? log(du) : R(0.0));
+        lg0 += HL(q) ? (HU(q) ? llog(dl * du) : llog(dl)) : (HU(q) ? llog(du) : R(0.0));
         if (rtype[q] < R_NONE) th0 += fabs(cr[q] - sr[q]);
         if (rtype[q] == R_OBJ) fo += cr[q];
     }
@@ -1685,9 +1685,9 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
         sl = wsum(sl);
         const R phi = uni(f_cur - mu * lsum_cur);
         const R gphi = uni(gdv - mu * sl);
-        // switching condition a (-gphi)^s_phi > theta^s_theta in log space: log a + s_phi log(-gphi) >
+        // switching condition a (-gphi)^s_phi > theta^s_theta in log space: log a + s_phi llog(-gphi) >
         // s_theta log theta (two logs per iteration instead of two pow per trial)
-        const R lsw = uni(gphi < 0 ? sth * log(theta) - sph * log(-gphi) : R(0.0));
+        const R lsw = uni(gphi < 0 ? sth * llog(theta) - sph * llog(-gphi) : R(0.0));
         R amin;
         if (gphi < 0) {
             amin = fmin(gth, gph * theta / -gphi);
@@ -1699,7 +1699,7 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
         STAMP(6);
         // ---- filter line search on trial points V + a dV (row registers only)
         R a = ap;
-        R la = uni(log(ap));   // log a, tracked exactly through the halvings
+        R la = uni(llog(ap));   // log a, tracked exactly through the halvings
         bool accepted = false, ftype = false;
         R ctr[RPL], ta0[RPL], ta1[RPL], vt[RPL][4];
         R ft = R(0.0), lgt = R(0.0);
@@ -1724,7 +1724,7 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
                 const R d1 = st - cl[q], d2 = cu[q] - st;
                 if (HL(q) && !(d1 > 0)) bad = true;
                 if (HU(q) && !(d2 > 0)) bad = true;
-                lgt += HL(q) ? (HU(q) ? log(d1 * d2) : log(d1)) : (HU(q) ? log(d2) : R(0.0));
+                lgt += HL(q) ? (HU(q) ? llog(d1 * d2) : llog(d1)) : (HU(q) ? llog(d2) : R(0.0));
             }
             wsum2(ft, tht);
             lgt = wsum(lgt);
@@ -1805,7 +1805,7 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
                     v = fmin(v, cu[q] - pu);
                 sr[q] = rtype[q] < R_NONE ? v : R(0.0);
                 const R d1 = sr[q] - cl[q], d2 = cu[q] - sr[q];
-                lr += HL(q) ? (HU(q) ? log(d1 * d2) : log(d1)) : (HU(q) ? log(d2) : R(0.0));
+                lr += HL(q) ? (HU(q) ? llog(d1 * d2) : llog(d1)) : (HU(q) ? llog(d2) : R(0.0));
                 if (rtype[q] == R_OBJ) fr += cr[q];
             }
             wsum2(fr, lr);
@@ -3097,6 +3097,219 @@ __global__ __launch_bounds__(256) void rollout_init_kernel(long long B, int S, i
 }
 
 // ------------------------------------------------------------------------------------------------
+// closed loop at the reference's control rate (alipmpc_closed_loop_batch): main_sim_mpc.py:41,65-135 driving
+// Logger.set_stf_head / gen_nex_foot_input (data_procs/logger_mpc.py:270-371) on an ALIP plant.  Per tick
+// i of step s (rest_t = T - i T / f_cyc):
+//   cl_project_kernel  tick 0: set_stf_head (tube_func, avg_hd -> hd_input_pr, hd_input_cos);
+//                      x_nex = get_next_states(plant, [stance foot, hd_input_pr], rest_t) (MPC_LIP_modi.py:149-178);
+//                      warm start: [x_nex] x 3 on the first call, else the previous plan x_mpc_tar (unshifted,
+//                      num_step >= 1 in the driver; sig_step: [g2..gN, gN] as solveMPCCBF does it)
+//   solve launch       od_ev = -leg_ind
+//   cl_update_kernel   nex_turn, mpc_hds_list, mpc_state_tar from the solve; the plant moves dt = T / f_cyc
+//                      around the stance foot (+ an optional seeded velocity kick: plant mismatch); after the
+//                      last tick: touchdown, stance foot <- p_list[0][0:2] of that solve, leg_ind <- -leg_ind,
+//                      and the episode stops if close_2_goal was reported before this tick (the driver's
+//                      real_close check precedes the close2goal update, main_sim_mpc.py:124-135)
+// ------------------------------------------------------------------------------------------------
+struct CLP {
+    long long B;
+    int S, f, s, i, variant, N;
+    double ch_r, shb_r, bsh_r, tr;   // ALIP flow over rest_t: cosh, sinh / beta, beta sinh, rest_t / T
+    double ch_d, shb_d, bsh_d, td;   // ... over dt = T / f_cyc
+    double kick;
+    unsigned long long seed;
+    const double* goal;
+    double* x;        // B x 5 plant state
+    double* pst;      // B x 2 stance foot
+    double* hdv;      // B x 4: nex_turn, hd_input_pr, hd_input_cos, -
+    double* mhd;      // B x 3 mpc_hds_list
+    double* plan;     // B x 5N mpc_state_tar
+    int8_t* leg;      // B leg_ind
+    uint8_t* flags;   // B: bit 0 active, bit 1 has a plan, bit 2 real_close
+    double* xs;       // solve inputs
+    double* u0;
+    int8_t* sleg;
+    const double* u;  // solve outputs
+    const double* foot;
+    const double* x_pred;
+    const int32_t* status;
+    const int32_t* iters;
+    uint8_t* active;  // the solve's active mask
+    double* foot_traj;      // B x S x 3
+    double* x_traj;         // B x (S+1) x 5
+    double* hd_traj;        // B x S x 2
+    int32_t* status_traj;   // B x S x f
+    int32_t* iters_traj;    // B x S x f
+    int32_t* steps_to_goal; // B
+};
+
+// Logger.angle_A_minus_B (logger_mpc.py:169-175)
+__host__ __device__ inline double ang_diff(double A, double B)
+{
+    double r = A - B;
+    if (r < 0 && fabs(r) > M_PI)
+        r += 2 * M_PI;
+    else if (r > 0 && fabs(r) > M_PI)
+        r -= 2 * M_PI;
+    return r;
+}
+// Logger.tube_func (logger_mpc.py:283-300)
+__host__ __device__ inline double tube_turn(double turning, double init)
+{
+    double tv = init;
+    if (turning > 0)
+        tv += (0.15 > turning ? 0.4 : 0.7) * turning;
+    else if (turning < 0)
+        tv += (-0.15 < turning ? 0.4 : 0.7) * turning;
+    return ang_diff(tv, init);
+}
+
+// splitmix64 -> uniform [0, 1): the plant's velocity kick of (episode, step, tick, axis)
+__host__ __device__ inline double cl_uniform(unsigned long long seed, long long b, int s, int i, int axis)
+{
+    unsigned long long z = seed + 0x9E3779B97F4A7C15ull *
+                                      (((((unsigned long long)b * 1048576ull + (unsigned long long)s) * 1024ull +
+                                         (unsigned long long)i) * 2ull + (unsigned long long)axis) + 1ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z = z ^ (z >> 31);
+    return (double)(z >> 11) * (1.0 / 9007199254740992.0);
+}
+
+__global__ __launch_bounds__(256) void cl_project_kernel(CLP C)
+{
+    const long long b = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= C.B) return;
+    const uint8_t fl = C.flags[b];
+    C.active[b] = fl & 1;
+    if (!(fl & 1)) return;
+    double* x = C.x + 5 * b;
+    double* hv = C.hdv + 4 * b;
+    const double* mh = C.mhd + 3 * b;
+    if (C.i == 0) {
+        // set_stf_head (logger_mpc.py:270-280) with the plant heading
+        const double cur = x[4];
+        hv[2] = cur;
+        hv[0] = tube_turn(hv[0], cur);
+        double sum = hv[0];
+        const double nc[3] = {cur, mh[0], mh[1]};
+        for (int k = 0; k < 3; ++k) sum += ang_diff(mh[k], nc[k]);
+        hv[1] = sum / 4.0;
+        if (C.hd_traj) {
+            C.hd_traj[((size_t)b * C.S + C.s) * 2] = hv[1];
+            C.hd_traj[((size_t)b * C.S + C.s) * 2 + 1] = hv[2];
+        }
+    }
+    // get_next_states(pos, vel, hd, [foot, hd_input_pr], rest_t)
+    const double fx = C.pst[2 * b], fy = C.pst[2 * b + 1], hp = hv[1];
+    double xn[5];
+    xn[0] = C.ch_r * x[0] + C.shb_r * x[2] + (1.0 - C.ch_r) * fx;
+    xn[1] = C.ch_r * x[1] + C.shb_r * x[3] + (1.0 - C.ch_r) * fy;
+    xn[2] = C.bsh_r * x[0] + C.ch_r * x[2] - C.bsh_r * fx;
+    xn[3] = C.bsh_r * x[1] + C.ch_r * x[3] - C.bsh_r * fy;
+    xn[4] = x[4] + C.tr * hp;
+    for (int c = 0; c < 5; ++c) C.xs[5 * b + c] = xn[c];
+    const int n = 5 * C.N;
+    double* g = C.u0 + (size_t)b * n;
+    const double* pl = C.plan + (size_t)b * n;
+    if (!(fl & 2)) {
+        for (int k = 0; k < C.N; ++k)
+            for (int c = 0; c < 5; ++c) g[5 * k + c] = xn[c];
+    } else if (C.variant == ALIPMPC_VARIANT_SIG_STEP) {
+        for (int k = 0; k < C.N; ++k) {
+            const int src = k + 1 < C.N ? k + 1 : C.N - 1;
+            for (int c = 0; c < 5; ++c) g[5 * k + c] = pl[5 * src + c];
+        }
+    } else {
+        for (int i = 0; i < n; ++i) g[i] = pl[i];
+    }
+    C.sleg[b] = (int8_t)(-C.leg[b]);
+}
+
+__global__ __launch_bounds__(256) void cl_update_kernel(CLP C)
+{
+    const long long b = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= C.B) return;
+    uint8_t fl = C.flags[b];
+    const size_t ti = ((size_t)b * C.S + C.s) * C.f + C.i;
+    if (!(fl & 1)) {
+        if (C.status_traj) C.status_traj[ti] = ALIPMPC_ROLLOUT_DONE;
+        if (C.iters_traj) C.iters_traj[ti] = 0;
+        if (C.i == C.f - 1) {
+            if (C.foot_traj)
+                for (int c = 0; c < 3; ++c) C.foot_traj[((size_t)b * C.S + C.s) * 3 + c] = NAN;
+            if (C.x_traj)
+                for (int c = 0; c < 5; ++c) C.x_traj[((size_t)b * (C.S + 1) + C.s + 1) * 5 + c] = C.x[5 * b + c];
+        }
+        return;
+    }
+    const int n = 5 * C.N;
+    if (C.status_traj) C.status_traj[ti] = C.status[b];
+    if (C.iters_traj) C.iters_traj[ti] = C.iters[b];
+    const double* ub = C.u + (size_t)b * n;
+    const double* xp = C.x_pred + (size_t)b * n;
+    for (int i = 0; i < n; ++i) C.plan[(size_t)b * n + i] = ub[i];
+    fl |= 2;
+    double* hv = C.hdv + 4 * b;
+    hv[0] = C.foot[3 * b + 2];   // nex_turn = nex_contr[2]
+    for (int k = 0; k < 3 && k < C.N; ++k) C.mhd[3 * b + k] = xp[5 * k + 4];
+    // close_2_goal of this solve (modi |pos_1 - goal| <= 0.15, MPC_LIP_modi.py:108-115; sig_step any step
+    // <= 0.35, MPC_LIP_sig_step.py:104-111)
+    const double gx_ = C.goal[2 * b], gy_ = C.goal[2 * b + 1];
+    bool close = false;
+    const int kmax = C.variant == ALIPMPC_VARIANT_SIG_STEP ? C.N : 1;
+    const double rad = C.variant == ALIPMPC_VARIANT_MODI ? 0.15 : 0.35;
+    for (int k = 0; k < kmax; ++k) {
+        const double dx = xp[5 * k] - gx_, dy = xp[5 * k + 1] - gy_;
+        close = close || sqrt(dx * dx + dy * dy) <= rad;
+    }
+    // the plant moves dt around the stance foot (+ the velocity kick)
+    double* x = C.x + 5 * b;
+    const double fx = C.pst[2 * b], fy = C.pst[2 * b + 1];
+    double xn[5];
+    xn[0] = C.ch_d * x[0] + C.shb_d * x[2] + (1.0 - C.ch_d) * fx;
+    xn[1] = C.ch_d * x[1] + C.shb_d * x[3] + (1.0 - C.ch_d) * fy;
+    xn[2] = C.bsh_d * x[0] + C.ch_d * x[2] - C.bsh_d * fx;
+    xn[3] = C.bsh_d * x[1] + C.ch_d * x[3] - C.bsh_d * fy;
+    xn[4] = x[4] + C.td * hv[1];
+    if (C.kick > 0) {
+        xn[2] += C.kick * (2.0 * cl_uniform(C.seed, b, C.s, C.i, 0) - 1.0);
+        xn[3] += C.kick * (2.0 * cl_uniform(C.seed, b, C.s, C.i, 1) - 1.0);
+    }
+    for (int c = 0; c < 5; ++c) x[c] = xn[c];
+    if (C.i == C.f - 1) {
+        // touchdown: the planned foothold becomes the stance foot, stance switch
+        C.pst[2 * b] = C.foot[3 * b];
+        C.pst[2 * b + 1] = C.foot[3 * b + 1];
+        C.leg[b] = (int8_t)(-C.leg[b]);
+        if (C.foot_traj)
+            for (int c = 0; c < 3; ++c) C.foot_traj[((size_t)b * C.S + C.s) * 3 + c] = C.foot[3 * b + c];
+        if (C.x_traj)
+            for (int c = 0; c < 5; ++c) C.x_traj[((size_t)b * (C.S + 1) + C.s + 1) * 5 + c] = xn[c];
+        if (fl & 4) {
+            fl &= (uint8_t)~1u;
+            if (C.steps_to_goal) C.steps_to_goal[b] = C.s + 1;
+        }
+    }
+    if (close) fl |= 4;
+    C.flags[b] = fl;
+}
+
+__global__ __launch_bounds__(256) void cl_init_kernel(CLP C)
+{
+    const long long b = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= C.B) return;
+    C.flags[b] = 1;
+    for (int k = 0; k < 4; ++k) C.hdv[4 * b + k] = 0.0;   // nex_turn = 0 (logger_mpc.py:90)
+    // mpc_hds_list = [0, 0, 0] in the Logger's robot frame, whose origin is the initial pose (logger_mpc.py:27):
+    // the initial heading in the map frame the plant and the MPC share here
+    for (int k = 0; k < 3; ++k) C.mhd[3 * b + k] = C.x[5 * b + 4];
+    if (C.steps_to_goal) C.steps_to_goal[b] = -1;
+    if (C.x_traj)
+        for (int c = 0; c < 5; ++c) C.x_traj[(size_t)b * (C.S + 1) * 5 + c] = C.x[5 * b + c];
+}
+
+// ------------------------------------------------------------------------------------------------
 // dense CoM traces of a plan (the pos_det output of MPCCBF.gen_control_test, MPC_LIP_modi.py:117-122,
 // 304-322): for step k, rows [x_k[0:2]; pos(t_i)], t_i = i * 0.01 (np.arange(0, dt + 0.01, 0.01)), of the
 // continuous ALIP flow from x_k around the stance foot p_k:  pos(t) = ch x_k[0:2] + sh/beta x_k[2:4] +
@@ -4144,6 +4357,139 @@ int alipmpc_rollout_batch(void* handle, int64_t B, int32_t S, const double* x0, 
         if (iters_traj) HIPCHK(h, hipMemcpyAsync(iters_traj, l.itt, Bz * Sz * 4, hipMemcpyDeviceToHost, st));
         if (steps_to_goal) HIPCHK(h, hipMemcpyAsync(steps_to_goal, l.sg, Bz * 4, hipMemcpyDeviceToHost, st));
         if (u_traj) HIPCHK(h, hipMemcpyAsync(u_traj, l.ut, Bz * Sz * n * 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(h, hipStreamSynchronize(st));
+    }
+    return ALIPMPC_OK;
+}
+
+int alipmpc_closed_loop_batch(void* handle, int64_t B, int32_t S, int32_t f_cyc, double kick, uint64_t seed,
+                              const double* x0, const double* foot0, const double* goal, const int8_t* leg,
+                              const double* cir, const int32_t* nc, const double* elp, const int32_t* ne,
+                              double* foot_traj, double* x_traj, double* hd_traj, int32_t* status_traj,
+                              int32_t* iters_traj, int32_t* steps_to_goal, void* hip_stream)
+{
+    Handle* h = (Handle*)handle;
+    if (!h) return ALIPMPC_EINVAL;
+    const alipmpc_cfg& cf = h->cfg;
+    if (cf.variant == ALIPMPC_VARIANT_DD) return fail(h, ALIPMPC_EUNSUPPORTED, "closed loop: LIP variants only");
+    if (B < 0 || S < 0 || f_cyc < 1 || !(kick >= 0)) return fail(h, ALIPMPC_EINVAL, "B, S < 0, f_cyc < 1 or kick < 0");
+    if (B == 0 || S == 0) return ALIPMPC_OK;
+    if (!x0 || !foot0 || !goal || !leg || !nc || (cf.nc_max > 0 && !cir) || (cf.ne_max > 0 && (!elp || !ne)))
+        return fail(h, ALIPMPC_EINVAL, "missing input pointer");
+    HIPCHK(h, hipSetDevice(h->device));
+    const int N = h->N, n = 5 * N;
+    const size_t Bz = (size_t)B, Sz = (size_t)S, Fz = (size_t)f_cyc;
+    hipStream_t st = stream_of(h, hip_stream);
+    const bool host = hip_stream == nullptr;
+    auto layout = [&](Carver& cv, bool take_io) {
+        struct L {
+            double *x, *pst, *hdv, *mhd, *plan, *xs, *u0, *u, *foot, *xp;
+            int8_t *leg, *sleg;
+            uint8_t *flags, *act;
+            int32_t *st, *it;
+            double *goal, *cir, *elp, *ft, *xt, *hd;
+            int32_t *nc, *ne, *stt, *itt, *sg;
+        } l{};
+        l.x = cv.take<double>(Bz * 5); l.pst = cv.take<double>(Bz * 2); l.hdv = cv.take<double>(Bz * 4);
+        l.mhd = cv.take<double>(Bz * 3); l.plan = cv.take<double>(Bz * n); l.xs = cv.take<double>(Bz * 5);
+        l.u0 = cv.take<double>(Bz * n); l.u = cv.take<double>(Bz * n); l.foot = cv.take<double>(Bz * 3);
+        l.xp = cv.take<double>(Bz * n); l.leg = cv.take<int8_t>(Bz); l.sleg = cv.take<int8_t>(Bz);
+        l.flags = cv.take<uint8_t>(Bz); l.act = cv.take<uint8_t>(Bz); l.st = cv.take<int32_t>(Bz);
+        l.it = cv.take<int32_t>(Bz);
+        if (take_io) {
+            l.goal = cv.take<double>(Bz * 2); l.cir = cv.take<double>(Bz * 3 * cf.nc_max);
+            l.elp = cv.take<double>(Bz * 5 * cf.ne_max); l.nc = cv.take<int32_t>(Bz); l.ne = cv.take<int32_t>(Bz);
+            l.ft = cv.take<double>(Bz * Sz * 3); l.xt = cv.take<double>(Bz * (Sz + 1) * 5);
+            l.hd = cv.take<double>(Bz * Sz * 2); l.stt = cv.take<int32_t>(Bz * Sz * Fz);
+            l.itt = cv.take<int32_t>(Bz * Sz * Fz); l.sg = cv.take<int32_t>(Bz);
+        }
+        return l;
+    };
+    size_t need;
+    {
+        Carver cv{nullptr};
+        layout(cv, host);
+        need = cv.off + 256;
+    }
+    if (h->rstage_bytes < need) {
+        if (h->rstage) hipFree(h->rstage);
+        h->rstage = nullptr;
+        h->rstage_bytes = 0;
+        HIPCHK(h, hipMalloc(&h->rstage, need));
+        h->rstage_bytes = need;
+    }
+    Carver cv{(char*)h->rstage};
+    auto l = layout(cv, host);
+    const hipMemcpyKind in_kind = host ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
+    HIPCHK(h, hipMemcpyAsync(l.x, x0, Bz * 5 * 8, in_kind, st));
+    HIPCHK(h, hipMemcpyAsync(l.pst, foot0, Bz * 2 * 8, in_kind, st));
+    HIPCHK(h, hipMemcpyAsync(l.leg, leg, Bz, in_kind, st));
+    const double *d_goal = goal, *d_cir = cir, *d_elp = elp;
+    const int32_t *d_nc = nc, *d_ne = ne;
+    double *d_ft = foot_traj, *d_xt = x_traj, *d_hd = hd_traj;
+    int32_t *d_stt = status_traj, *d_itt = iters_traj, *d_sg = steps_to_goal;
+    if (host) {
+        HIPCHK(h, hipMemcpyAsync(l.goal, goal, Bz * 2 * 8, hipMemcpyHostToDevice, st));
+        if (cf.nc_max) HIPCHK(h, hipMemcpyAsync(l.cir, cir, Bz * 3 * cf.nc_max * 8, hipMemcpyHostToDevice, st));
+        HIPCHK(h, hipMemcpyAsync(l.nc, nc, Bz * 4, hipMemcpyHostToDevice, st));
+        if (cf.ne_max) {
+            HIPCHK(h, hipMemcpyAsync(l.elp, elp, Bz * 5 * cf.ne_max * 8, hipMemcpyHostToDevice, st));
+            HIPCHK(h, hipMemcpyAsync(l.ne, ne, Bz * 4, hipMemcpyHostToDevice, st));
+        }
+        d_goal = l.goal; d_cir = l.cir; d_nc = l.nc;
+        d_elp = cf.ne_max ? l.elp : nullptr;
+        d_ne = cf.ne_max ? l.ne : nullptr;
+        d_ft = foot_traj ? l.ft : nullptr; d_xt = x_traj ? l.xt : nullptr; d_hd = hd_traj ? l.hd : nullptr;
+        d_stt = status_traj ? l.stt : nullptr; d_itt = iters_traj ? l.itt : nullptr;
+        d_sg = steps_to_goal ? l.sg : nullptr;
+    }
+    CLP C;
+    std::memset(&C, 0, sizeof(C));
+    C.B = B; C.S = S; C.f = f_cyc; C.variant = cf.variant; C.N = N; C.kick = kick; C.seed = (unsigned long long)seed;
+    C.goal = d_goal; C.x = l.x; C.pst = l.pst; C.hdv = l.hdv; C.mhd = l.mhd; C.plan = l.plan; C.leg = l.leg;
+    C.flags = l.flags; C.xs = l.xs; C.u0 = l.u0; C.sleg = l.sleg; C.u = l.u; C.foot = l.foot; C.x_pred = l.xp;
+    C.status = l.st; C.iters = l.it; C.active = l.act;
+    C.foot_traj = d_ft; C.x_traj = d_xt; C.hd_traj = d_hd; C.status_traj = d_stt; C.iters_traj = d_itt;
+    C.steps_to_goal = d_sg;
+    const double beta = std::sqrt(cf.g / cf.H), T = cf.dt, dt = T / f_cyc;
+    C.ch_d = std::cosh(beta * dt); C.shb_d = std::sinh(beta * dt) / beta; C.bsh_d = std::sinh(beta * dt) * beta;
+    C.td = dt / T;
+    const unsigned g1 = (unsigned)((B + 255) / 256);
+    hipLaunchKernelGGL(cl_init_kernel, dim3(g1), dim3(256), 0, st, C);
+    HIPCHK(h, hipGetLastError());
+    KP P = make_kp(h, B, true);
+    P.goal = d_goal; P.cir = d_cir; P.nc = d_nc; P.elp = d_elp; P.ne = d_ne;
+    P.x0 = l.xs; P.leg = l.sleg; P.u0 = l.u0; P.active = l.act;
+    P.u_out = l.u; P.foot_out = l.foot; P.x_pred = l.xp; P.status = l.st; P.iters = l.it;
+    const int ei = h->evi;
+    h->evi = (ei + 1) % Handle::NEV;
+    HIPCHK(h, hipEventRecord(h->ev[ei][0], st));
+    for (int s = 0; s < S; ++s) {
+        for (int i = 0; i < f_cyc; ++i) {
+            // rest_t = step_t - i * (step_t / f_cyc)   (main_sim_mpc.py:78)
+            const double rest = T - i * (T / f_cyc);
+            C.s = s;
+            C.i = i;
+            C.ch_r = std::cosh(beta * rest); C.shb_r = std::sinh(beta * rest) / beta;
+            C.bsh_r = std::sinh(beta * rest) * beta; C.tr = rest * (1.0 / T);
+            hipLaunchKernelGGL(cl_project_kernel, dim3(g1), dim3(256), 0, st, C);
+            HIPCHK(h, hipGetLastError());
+            P.queue = h->dq + 2 * (h->qi.fetch_add(1u) % Handle::NQ);
+            HIPCHK(h, launch(h, true, P, st));
+            hipLaunchKernelGGL(cl_update_kernel, dim3(g1), dim3(256), 0, st, C);
+            HIPCHK(h, hipGetLastError());
+        }
+    }
+    HIPCHK(h, hipEventRecord(h->ev[ei][1], st));
+    h->evlast = ei;
+    h->timed = true;
+    if (host) {
+        if (foot_traj) HIPCHK(h, hipMemcpyAsync(foot_traj, l.ft, Bz * Sz * 3 * 8, hipMemcpyDeviceToHost, st));
+        if (x_traj) HIPCHK(h, hipMemcpyAsync(x_traj, l.xt, Bz * (Sz + 1) * 5 * 8, hipMemcpyDeviceToHost, st));
+        if (hd_traj) HIPCHK(h, hipMemcpyAsync(hd_traj, l.hd, Bz * Sz * 2 * 8, hipMemcpyDeviceToHost, st));
+        if (status_traj) HIPCHK(h, hipMemcpyAsync(status_traj, l.stt, Bz * Sz * Fz * 4, hipMemcpyDeviceToHost, st));
+        if (iters_traj) HIPCHK(h, hipMemcpyAsync(iters_traj, l.itt, Bz * Sz * Fz * 4, hipMemcpyDeviceToHost, st));
+        if (steps_to_goal) HIPCHK(h, hipMemcpyAsync(steps_to_goal, l.sg, Bz * 4, hipMemcpyDeviceToHost, st));
         HIPCHK(h, hipStreamSynchronize(st));
     }
     return ALIPMPC_OK;

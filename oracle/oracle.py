@@ -234,3 +234,138 @@ def rollout_batch(cfg, x0, goal, leg, cir, nc, elp, ne, u0, last_u=None, steps=8
             stg[done] = t + 1
         xs[:, t + 1] = x
     return dict(foot=foot, x=xs, status=status, iters=iters, steps_to_goal=stg, u=uts)
+
+
+# ---------------------------------------------------------------- closed loop at the control rate (test oracle)
+def _ang_diff(A, B):
+    """Logger.angle_A_minus_B (data_procs/logger_mpc.py:169-175)."""
+    r = A - B
+    if r < 0 and abs(r) > math.pi:
+        r += 2 * math.pi
+    elif r > 0 and abs(r) > math.pi:
+        r -= 2 * math.pi
+    return r
+
+
+def _tube_turn(turning, init):
+    """Logger.tube_func (data_procs/logger_mpc.py:283-300)."""
+    tv = init
+    if turning > 0:
+        tv += (0.4 if 0.15 > turning else 0.7) * turning
+    elif turning < 0:
+        tv += (0.4 if -0.15 < turning else 0.7) * turning
+    return _ang_diff(tv, init)
+
+
+_M64 = (1 << 64) - 1
+
+
+def cl_uniform(seed, b, s, i, axis):
+    """splitmix64 uniform [0, 1) of (episode, step, tick, axis): the closed loop's velocity kicks (the same
+    integer recipe as cl_uniform in csrc/alipmpc.hip)."""
+    key = ((((b * 1048576 + s) * 1024 + i) * 2 + axis) + 1) & _M64
+    z = (seed + 0x9E3779B97F4A7C15 * key) & _M64
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & _M64
+    z = z ^ (z >> 31)
+    return (z >> 11) * (1.0 / 9007199254740992.0)
+
+
+def closed_loop_batch(cfg, x0, foot0, goal, leg, cir, nc, elp=None, ne=None, steps=8, f_cyc=40, kick=0.0, seed=0,
+                      nthreads=8):
+    """Oracle of alipmpc_closed_loop_batch (include/alipmpc.h): the reference driver's per-tick loop
+    (main_sim_mpc.py:65-135; Logger.set_stf_head / gen_nex_foot_input, data_procs/logger_mpc.py:270-371) on an
+    ALIP plant, every solve by the C oracle."""
+    N, n = cfg.N, 5 * cfg.N
+    x = np.array(x0, np.float64).reshape(-1, 5).copy()
+    B = len(x)
+    pst = np.array(foot0, np.float64).reshape(B, 2).copy()
+    goal = np.ascontiguousarray(np.broadcast_to(np.asarray(goal, np.float64), (B, 2)))
+    legv = np.array(leg, np.int8).reshape(B).copy()
+    hdv = np.zeros((B, 3))     # nex_turn, hd_input_pr, hd_input_cos
+    mhd = np.repeat(x[:, 4:5], 3, axis=1)   # mpc_hds_list: 0 in the Logger's robot frame = the initial heading here
+    plan = np.zeros((B, n))
+    active = np.ones(B, bool)
+    has_plan = np.zeros(B, bool)
+    rclose = np.zeros(B, bool)
+    S, F = int(steps), int(f_cyc)
+    beta, T = math.sqrt(cfg.g / cfg.H), cfg.dt
+    dt = T / F
+    ch_d, shb_d, bsh_d, td = math.cosh(beta * dt), math.sinh(beta * dt) / beta, math.sinh(beta * dt) * beta, dt / T
+    foot = np.full((B, S, 3), np.nan)
+    xs = np.zeros((B, S + 1, 5))
+    xs[:, 0] = x
+    hd = np.zeros((B, S, 2))
+    status = np.full((B, S, F), -10, np.int32)
+    iters = np.zeros((B, S, F), np.int32)
+    stg = np.full(B, -1, np.int32)
+    cir = np.asarray(cir)
+    nc = np.asarray(nc)
+    for s in range(S):
+        for i in range(F):
+            idx = np.nonzero(active)[0]
+            if len(idx) == 0:
+                continue
+            rest = T - i * (T / F)
+            ch_r, shb_r, bsh_r, tr = math.cosh(beta * rest), math.sinh(beta * rest) / beta, \
+                math.sinh(beta * rest) * beta, rest * (1.0 / T)
+            if i == 0:
+                for b in idx:
+                    cur = x[b, 4]
+                    hdv[b, 2] = cur
+                    hdv[b, 0] = _tube_turn(hdv[b, 0], cur)
+                    ssum = hdv[b, 0]
+                    ncur = [cur, mhd[b, 0], mhd[b, 1]]
+                    for k in range(3):
+                        ssum += _ang_diff(mhd[b, k], ncur[k])
+                    hdv[b, 1] = ssum / 4.0
+                    hd[b, s] = hdv[b, 1], hdv[b, 2]
+            xi, fx, fy, hp = x[idx], pst[idx, 0], pst[idx, 1], hdv[idx, 1]
+            xn = np.stack([ch_r * xi[:, 0] + shb_r * xi[:, 2] + (1.0 - ch_r) * fx,
+                           ch_r * xi[:, 1] + shb_r * xi[:, 3] + (1.0 - ch_r) * fy,
+                           bsh_r * xi[:, 0] + ch_r * xi[:, 2] - bsh_r * fx,
+                           bsh_r * xi[:, 1] + ch_r * xi[:, 3] - bsh_r * fy,
+                           xi[:, 4] + tr * hp], axis=1)
+            u0 = np.tile(xn, (1, N))
+            hp_ = has_plan[idx]
+            if cfg.variant == VARIANT_SIG_STEP:
+                pb = plan[idx].reshape(len(idx), N, 5)
+                sh = np.concatenate([pb[:, 1:], pb[:, -1:]], axis=1).reshape(len(idx), n)
+                u0[hp_] = sh[hp_]
+            else:
+                u0[hp_] = plan[idx][hp_]
+            sub = lambda a: None if a is None else np.asarray(a)[idx]  # noqa: E731
+            o = solve_batch(cfg, xn, goal[idx], -legv[idx], cir[idx], nc[idx], sub(elp), sub(ne), u0,
+                            nthreads=nthreads)
+            status[idx, s, i] = o["status"]
+            iters[idx, s, i] = o["iters"]
+            plan[idx] = o["u"]
+            has_plan[idx] = True
+            hdv[idx, 0] = o["foot"][:, 2]
+            xp = o["x_pred"]
+            mhd[idx] = xp[:, :3, 4]
+            d = np.sqrt(((xp[:, :, 0:2] - goal[idx, None, :]) ** 2).sum(-1))
+            if cfg.variant == VARIANT_SIG_STEP:
+                close = (d <= 0.35).any(1)
+            else:
+                close = d[:, 0] <= (0.15 if cfg.variant == VARIANT_MODI else 0.35)
+            xa = np.stack([ch_d * xi[:, 0] + shb_d * xi[:, 2] + (1.0 - ch_d) * fx,
+                           ch_d * xi[:, 1] + shb_d * xi[:, 3] + (1.0 - ch_d) * fy,
+                           bsh_d * xi[:, 0] + ch_d * xi[:, 2] - bsh_d * fx,
+                           bsh_d * xi[:, 1] + ch_d * xi[:, 3] - bsh_d * fy,
+                           xi[:, 4] + td * hp], axis=1)
+            if kick > 0:
+                for j, b in enumerate(idx):
+                    xa[j, 2] += kick * (2.0 * cl_uniform(seed, int(b), s, i, 0) - 1.0)
+                    xa[j, 3] += kick * (2.0 * cl_uniform(seed, int(b), s, i, 1) - 1.0)
+            x[idx] = xa
+            if i == F - 1:
+                pst[idx] = o["foot"][:, 0:2]
+                legv[idx] = -legv[idx]
+                foot[idx, s] = o["foot"]
+                stop = idx[rclose[idx]]
+                active[stop] = False
+                stg[stop] = s + 1
+            rclose[idx] |= close
+        xs[:, s + 1] = x
+    return dict(foot=foot, x=xs, hd=hd, status=status, iters=iters, steps_to_goal=stg)

@@ -811,3 +811,49 @@ def test_lane_program_unsupported_shapes(gpu_lib):
             gpu_lib.Solver(cfg)
     with pytest.raises(RuntimeError, match="EUNSUPPORTED"):
         gpu_lib.Solver(gpu_lib.default_cfg(gpu_lib.VARIANT_DD, 3, nc_max=5, ne_max=0, program=gpu_lib.PROGRAM_LANE))
+
+
+# ---------------------------------------------------------------- closed loop at the control rate
+@pytest.mark.parametrize("variant,kick,program", [(0, 0.0, 0), (0, 0.05, 0), (1, 0.05, 0), (0, 0.05, 1)])
+def test_closed_loop_matches_oracle(gpu_lib, coracle, variant, kick, program):
+    """alipmpc_closed_loop_batch (f_cyc = 40 solves per walking step, heading tube + avg_hd at each touchdown,
+    get_next_states projection at rest_t = T - i T / 40, warm start from the previous plan, stance switch and
+    close-to-goal stop as main_sim_mpc.py:65-135) against oracle.closed_loop_batch on the same seeded episodes:
+    per-tick statuses, iteration counts, steps to the goal and converged touchdown footholds agree on the large
+    majority of ticks / steps (each tick warm-starts from the previous plan, so a rounding-level difference can
+    change an iteration count or move an unconverged iterate, and the episode then drifts)."""
+    from alipmpc import scenes
+    B, S, F = 48, 4, 40
+    bt = scenes.make_batch(B, seed=520 + variant + int(kick * 100), n_cir=5)
+    x0 = bt["x0"].copy()
+    x0[:12, 0:2] = bt["goal"][:12] - (np.array([1.0, 0.8]) if variant == 1 else np.array([0.6, 0.5]))
+    leg = bt["leg"].astype(np.int8)
+    # a consistent start: x0 is the state as the stance switches onto the first planned foothold of a solve from
+    # x0 (the MPC's x_1 = flow of x0 about u_0 over T), leg the parity that solve was posed with
+    co = coracle.default_cfg(variant, 3, nc_max=5, ne_max=0)
+    foot0 = coracle.solve_batch(co, x0, bt["goal"], leg, bt["cir"], bt["nc"], None, None,
+                                np.tile(x0, (1, 3)))["foot"][:, 0:2]
+    cfg = gpu_lib.default_cfg(variant, 3, nc_max=5, ne_max=0, program=program)
+    o = gpu_lib.Solver(cfg).closed_loop(x0, foot0, bt["goal"], leg, bt["cir"], bt["nc"], steps=S, f_cyc=F,
+                                        kick=kick, seed=7)
+    ref = coracle.closed_loop_batch(co, x0, foot0, bt["goal"], leg, bt["cir"], bt["nc"], steps=S, f_cyc=F, kick=kick,
+                                    seed=7)
+    assert o["status"].shape == (B, S, F)
+    # tick level: a warm-started solve sitting on the tolerance boundary may take one iteration more or less
+    # (or, rarely, end on another status) than the oracle's
+    assert (o["status"] == ref["status"]).mean() >= 0.98
+    assert (np.abs(o["iters"] - ref["iters"]) <= 1).mean() >= 0.98
+    # episode level: the same number of steps to the goal
+    assert (o["steps_to_goal"] == ref["steps_to_goal"]).mean() >= 0.9
+    # touchdown footholds of steps whose last solve converged on both sides
+    err = np.abs(o["foot"] - ref["foot"]).max(-1)
+    conv = (o["status"][:, :, -1] == 0) & (ref["status"][:, :, -1] == 0)
+    assert conv.sum() >= 0.4 * B * S
+    assert (err[conv] <= 1e-3).mean() >= 0.9 and np.median(err[conv]) <= 1e-6
+    # the first step's heading inputs depend on the initial state alone
+    np.testing.assert_allclose(o["hd"][:, 0], ref["hd"][:, 0], rtol=0, atol=1e-12)
+    np.testing.assert_allclose(o["x"][:, 0], x0, rtol=0, atol=0)
+    assert (o["steps_to_goal"][:12] > 0).sum() >= 4
+    done = o["status"] == gpu_lib.ROLLOUT_DONE
+    for b in np.nonzero(o["steps_to_goal"] > 0)[0]:
+        assert done[b, o["steps_to_goal"][b]:].all() and not done[b, :o["steps_to_goal"][b]].any()

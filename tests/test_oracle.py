@@ -301,3 +301,46 @@ def test_rollout_oracle_semantics(coracle, variant):
     for b in np.nonzero(reached)[0]:
         k = ro["steps_to_goal"][b]
         assert (ro["status"][b, k:] == -10).all() and (ro["status"][b, :k] != -10).all()
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+def test_closed_loop_oracle_semantics(coracle, variant):
+    """Closed loop at the control rate (main_sim_mpc.py:65-135): tick 0 solves at
+    get_next_states(x, stance, rest_t = T) with od_ev = -leg_ind and the warm start [x_nex] x 3; the plant's f_cyc
+    flows of T / f_cyc compose to one flow over T about the stance foot with the step's heading input hd_pr
+    (= 0 on the first step: mpc_hds_list starts at the initial heading); touchdown moves the stance to the last
+    solve's first foothold; an episode stops after the step on which close_2_goal first held."""
+    import math
+    from alipmpc import scenes
+    from alipmpc.planner import next_state
+    B, S, F = 16, 3, 8
+    bt = scenes.make_batch(B, seed=41 + variant, n_cir=3)
+    cfg = coracle.default_cfg(variant, 3, nc_max=3, ne_max=0)
+    x0 = bt["x0"].copy()
+    x0[:4, 0:2] = bt["goal"][:4] - np.array([0.5, 0.4])
+    leg = bt["leg"].astype(np.int8)
+    foot0 = coracle.solve_batch(cfg, x0, bt["goal"], leg, bt["cir"], bt["nc"], None, None,
+                                np.tile(x0, (1, 3)))["foot"][:, 0:2]
+    r = coracle.closed_loop_batch(cfg, x0, foot0, bt["goal"], leg, bt["cir"], bt["nc"], steps=S, f_cyc=F, nthreads=4)
+    beta = math.sqrt(9.81)
+    assert np.array_equal(r["hd"][:, 0, 0], np.zeros(B)) and np.array_equal(r["hd"][:, 0, 1], x0[:, 4])
+    xn0 = np.stack([next_state(beta, 0.4, x0[b, 0:2], x0[b, 2:4], x0[b, 4], [*foot0[b], 0.0], 0.4)[0]
+                    for b in range(B)])
+    first = coracle.solve_batch(cfg, xn0, bt["goal"], -leg, bt["cir"], bt["nc"], None, None, np.tile(xn0, (1, 3)))
+    assert np.array_equal(r["status"][:, 0, 0], first["status"])
+    assert np.array_equal(r["iters"][:, 0, 0], first["iters"])
+    for b in range(B):
+        stance = foot0[b]
+        for s in range(S):
+            if r["status"][b, s, 0] == -10:
+                assert (r["status"][b, s] == -10).all() and np.array_equal(r["x"][b, s + 1], r["x"][b, s])
+                continue
+            xs = r["x"][b, s]
+            xn, _ = next_state(beta, 0.4, xs[0:2], xs[2:4], xs[4], [*stance, r["hd"][b, s, 0]], 0.4)
+            assert np.allclose(xn, r["x"][b, s + 1], rtol=0, atol=1e-9)
+            stance = r["foot"][b, s, 0:2]
+    reached = r["steps_to_goal"] > 0
+    assert reached[:4].any()
+    for b in np.nonzero(reached)[0]:
+        k = r["steps_to_goal"][b]
+        assert (r["status"][b, k:] == -10).all() and (r["status"][b, :k] != -10).all()
