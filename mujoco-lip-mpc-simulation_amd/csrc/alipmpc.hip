@@ -330,62 +330,6 @@ struct Mfma<float> {
     __device__ static __forceinline__ int row(int g4, int i) { return 4 * g4 + i; }
 };
 
-// ------------------------------------------------------------------------------------------------
-// per-wave LDS workspace
-// ------------------------------------------------------------------------------------------------
-template <int N>
-struct WS {
-    typedef double real;
-    double* V;      // NG  current generator values
-    double* Vt;     // NG  trial values
-    double* dV;     // NG  step
-    double* gfg;    // NG  d f / d V
-    double* CT;     // N+1 cos(theta_k)  (of the V last passed to state_pass)
-    double* ST;     // N+1
-    double* S;      // (N+1) x 64 Hessian blocks
-    double* rcoef;  // mr4 x 4
-    double* ry;     // mr4
-    double* rsig;   // mr4
-    double* rw;     // mr4
-    double* obs;    // circles 3*nc_max, ellipses 5*ne_max, then qa, qb, qc, ek (4*ne_max)
-    double* K;      // NCP x KLD
-    uint8_t* rgen;  // mr4 x 4
-    int* nsel;      // [0] = nc_sel, [1] = ne_sel
-};
-
-// per-wave LDS doubles (16-byte multiple)
-template <int N>
-__host__ __device__ constexpr int ws_doubles(int nc_max, int ne_max, int mr4)
-{
-    int d = 4 * Dim<N>::NG + 2 * (N + 1) + 64 * (N + 1) + 7 * mr4 + 3 * nc_max + 9 * ne_max +
-            Dim<N>::NCP * Dim<N>::KLD + (4 * mr4 + 7) / 8 + 1;
-    return (d + 1) & ~1;
-}
-
-template <int N>
-__device__ WS<N> carve(double* base, int nc_max, int ne_max, int mr4)
-{
-    using D = Dim<N>;
-    WS<N> w;
-    double* p = base;
-    w.V = p; p += D::NG;
-    w.Vt = p; p += D::NG;
-    w.dV = p; p += D::NG;
-    w.gfg = p; p += D::NG;
-    w.CT = p; p += N + 1;
-    w.ST = p; p += N + 1;
-    w.S = p; p += 64 * (N + 1);
-    w.rcoef = p; p += 4 * mr4;
-    w.ry = p; p += mr4;
-    w.rsig = p; p += mr4;
-    w.rw = p; p += mr4;
-    w.obs = p; p += 3 * nc_max + 9 * ne_max;
-    w.K = p; p += D::NCP * D::KLD;
-    w.nsel = reinterpret_cast<int*>(p); p += 1;
-    w.rgen = reinterpret_cast<uint8_t*>(p);
-    return w;
-}
-
 // generator row indices
 __device__ __forceinline__ int gx(int k, int c) { return 8 * k + c; }       // state x_k comp c
 __device__ __forceinline__ int gp(int k, int c) { return 8 * k + 5 + c; }   // foothold p_k comp c
@@ -572,58 +516,11 @@ __device__ double row_eval(const KP& P, const RowInfo& ri, const double* V, cons
 }
 
 // ------------------------------------------------------------------------------------------------
-// state pass: lanes 1..N own state x_k.  Writes CT/ST for the given V; returns this lane's cost term
-// (0 elsewhere).  If GRAD, writes d f / d V into gfg (all NG entries).
-// ------------------------------------------------------------------------------------------------
-template <int N, bool GRAD>
-__device__ double state_pass(const KP& P, const double* V, double* CT, double* ST, double* gfg, double gxg, double gyg)
-{
-    const int lane = lane_id();
-    double fk = 0.0;
-    if (GRAD) {
-        for (int t = lane; t < Dim<N>::NG; t += WAVE) gfg[t] = 0.0;
-        wave_sync();
-    }
-    if (lane >= 1 && lane <= N) {
-        const int k = lane;
-        double th = V[gx(k, 4)];
-        double s_, c_;
-        sincos(th, &s_, &c_);
-        CT[k] = c_;
-        ST[k] = s_;
-        double px = V[gx(k, 0)], py = V[gx(k, 1)];
-        double w = P.q + (k == 1 ? P.p : 0.0);
-        double ex = px - gxg, ey = py - gyg;
-        double dxg = gxg - px, dyg = gyg - py;
-        double phi = th - atan2(dyg, dxg);
-        fk = w * (ex * ex + ey * ey) + P.r * phi * phi;
-        if (GRAD) {
-            double rho2 = dxg * dxg + dyg * dyg;
-            gfg[gx(k, 0)] = 2 * w * ex + 2 * P.r * phi * (-dyg / rho2);
-            gfg[gx(k, 1)] = 2 * w * ey + 2 * P.r * phi * (dxg / rho2);
-            gfg[gx(k, 4)] = 2 * P.r * phi;
-        }
-    }
-    return fk;
-}
-
-
-// J[r][col] from the generator form
-__device__ __forceinline__ double jrow_col(const double* rcoef, const uint8_t* rgen, const double* G, int ldg, int r,
-                                           int col)
-{
-    const double* cf = rcoef + 4 * r;
-    const uint8_t* gn = rgen + 4 * r;
-    return cf[0] * G[gn[0] * ldg + col] + cf[1] * G[gn[1] * ldg + col] + cf[2] * G[gn[2] * ldg + col] +
-           cf[3] * G[gn[3] * ldg + col];
-}
-
-// ------------------------------------------------------------------------------------------------
-// instance prologue: load inputs, select_obs, detour goal, ellipse forms, V = E x0 + G u0.
+// solve-instance prologue: load inputs, select_obs, detour goal, ellipse forms, V = E x0 + G p0.
 // Computed in fp64 for either workspace type (the discrete select/detour decisions do not depend on
 // cfg.precision); results are stored into the workspace's type.
 // ------------------------------------------------------------------------------------------------
-template <int N, bool FROM_U, class WT>
+template <int N, class WT>
 __device__ void prologue(const KP& P, const WT& w, const typename WT::real* G, const typename WT::real* E,
                          long long b, double& gxg, double& gyg, int& legv, double& uj)
 {
@@ -719,8 +616,7 @@ __device__ void prologue(const KP& P, const WT& w, const typename WT::real* G, c
             gyg = bcast(ny, first);
         }
     }
-    // FROM_U (eval): V = E x0 + G u with the u-tables staged in LDS.
-    // solve: warm start p0 = rows p_k of (Eu x0 + Gu u0) — the rollout of the reference's u0 — then
+    // warm start p0 = rows p_k of (Eu x0 + Gu u0) — the rollout of the reference's u0 — then
     // V = E x0 + G p0 with the foothold tables.
     constexpr int nu = D::nu;
     const double u0v = lane < nu ? P.u0[(size_t)b * nu + lane] : 0.0;
@@ -730,20 +626,6 @@ __device__ void prologue(const KP& P, const WT& w, const typename WT::real* G, c
     for (int c = 0; c < 5; ++c) xb[c] = bcast(xv, c);
     if (lane < nu) w.Vt[lane] = u0v;
     wave_sync();
-    if (FROM_U) {
-        for (int t = lane; t < D::NG; t += WAVE) {
-            double v = 0.0;
-#pragma unroll
-            for (int c = 0; c < 5; ++c) v += E[t * 5 + c] * xb[c];
-            const auto* gr = G + t * D::NCPU;
-#pragma unroll
-            for (int j = 0; j < nu; ++j) v += gr[j] * w.Vt[j];
-            w.V[t] = v;
-        }
-        uj = 0.0;
-        wave_sync();
-        return;
-    }
     if (lane < D::n) {
         const int t = 8 * (lane / 3) + 5 + lane % 3;      // generator row of p_k[c]
         double v = 0.0;
@@ -1205,7 +1087,7 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
 
     double gxg, gyg, uj;
     int legv;
-    prologue<N, false>(P, w, G, E, b, gxg, gyg, legv, uj);
+    prologue<N>(P, w, G, E, b, gxg, gyg, legv, uj);
     const int nc_sel = w.nsel[0], ne_sel = w.nsel[1];
     // unified quadratic forms per obstacle row slot (zero form for unused slots)
     {
@@ -1956,19 +1838,283 @@ __global__ __launch_bounds__(256, (solve_waves<KSM, R>())) void solve_kernel(KP 
 #include "lane_solve.inc"
 
 // ------------------------------------------------------------------------------------------------
-// eval kernel ("Jacobian sweep"): f, grad f, c, J, cl, cu, goal_eff, row_active at given u
+// eval kernel ("Jacobian sweep"): f, grad f, c, J, cl, cu, goal_eff, row_active at given u.
+//   One instance per 16-lane group (4 instances per wave, 16 per 256-thread workgroup): the per-instance
+//   set-up (select_obs ballots, detour, the rollout V = E x0 + G u, the N sin/cos/atan2 of the state pass)
+//   runs on a few lanes of each group at once, so its instruction stream is shared by 4 instances instead
+//   of being paid per wave; lane t of a group owns rows t, t + 16, ... and J columns t (+ 16), and a J row
+//   store is 4 contiguous 15-double runs (the rows of one instance are adjacent, so an instance's J block is
+//   written front to back).
 // ------------------------------------------------------------------------------------------------
+constexpr int GLANES = 16;                          // lanes per instance (one DPP row)
+constexpr int GROUPS_PER_BLOCK = WAVE * WAVES_PER_BLOCK / GLANES;
+
+// per-group eval workspace (doubles)
 template <int N>
-__global__ __launch_bounds__(256, 4) void eval_kernel(KP Pv)
+struct GWS {
+    double* rcoef;  // mr4 x 4
+    uint8_t* rgen;  // mr4 x 4
+    double* V;      // NG
+    double* gfg;    // NG   d f / d V
+    double* CT;     // N+1
+    double* ST;     // N+1
+    double* uv;     // nu   the instance's u
+    double* obs;    // circles 3*nc_max, ellipses 5*ne_max, then qa, qb, qc, ek (4*ne_max)
+};
+// the group stride is 4 (mod 16) doubles: the 4 groups of a wave read their rcoef rows (32-byte broadcasts)
+// from disjoint LDS banks
+template <int N>
+__host__ __device__ constexpr int gws_doubles(int nc_max, int ne_max, int mr4)
+{
+    const int d = 4 * mr4 + mr4 / 2 + 2 * Dim<N>::NG + 2 * (N + 1) + Dim<N>::nu + 3 * nc_max + 9 * ne_max;
+    return d + ((4 - d) % 16 + 16) % 16;
+}
+template <int N>
+__device__ GWS<N> carve_g(double* p, int nc_max, int ne_max, int mr4)
+{
+    GWS<N> w;
+    w.rcoef = p; p += 4 * mr4;   // 32-byte rows
+    w.rgen = reinterpret_cast<uint8_t*>(p); p += mr4 / 2;   // mr4 is a multiple of 4: 16-byte row quads
+    w.V = p; p += Dim<N>::NG;
+    w.gfg = p; p += Dim<N>::NG;
+    w.CT = p; p += N + 1;
+    w.ST = p; p += N + 1;
+    w.uv = p; p += Dim<N>::nu;
+    w.obs = p;
+    return w;
+}
+
+// global-memory views of output pointers (plain pointers read from the LDS copy of KP would be flat
+// accesses, whose stores also hold the LDS counter that every following LDS wait drains)
+typedef __attribute__((address_space(1))) double gdouble;
+typedef __attribute__((address_space(1))) int8_t gint8;
+__device__ __forceinline__ gdouble* gptr(double* p) { return (gdouble*)p; }
+__device__ __forceinline__ gint8* gptr(int8_t* p) { return (gint8*)p; }
+__device__ __forceinline__ const gdouble* gptr(const double* p) { return (const gdouble*)p; }
+
+// the 16 ballot bits of this lane's group
+__device__ __forceinline__ unsigned gballot(bool x)
+{
+    return (unsigned)(__ballot(x) >> (threadIdx.x & (WAVE - GLANES))) & 0xFFFFu;
+}
+// sum over the 16 lanes of a DPP row (every lane receives it)
+__device__ __forceinline__ double gsum16(double v)
+{
+    v += dpp<0xB1>(v);
+    v += dpp<0x4E>(v);
+    v += dpp<0x141>(v);
+    v += dpp<0x140>(v);
+    return v;
+}
+
+template <int N>
+__device__ __forceinline__ void eval_group_one(const KP& P, const GWS<N>& w, const double* G, const double* E, long long b,
+                                               int t)
 {
     using D = Dim<N>;
-    constexpr int n = D::nu;       // the reference callbacks are functions of u
-    constexpr int NT = D::NTU;
+    constexpr int nu = D::nu, NTU = D::NTU, NCP = D::NCPU, NG = D::NG;
+    const gdouble* x0 = gptr(P.x0) + 5 * b;
+    const int legv = P.leg[b];
+    const int ncr = P.nc[b];
+    const int ner = P.ne ? P.ne[b] : 0;
+    const double x0v0 = x0[0], x0v1 = x0[1];
+    const double g0 = gptr(P.goal)[2 * b], g1 = gptr(P.goal)[2 * b + 1];
+    // select_obs (MPC_LIP_modi.py:325-338): keep order, compact into the first slots (16 slots per pass)
+    int ncs = 0, nes = 0;
+    for (int base = 0; base < P.nc_max; base += GLANES) {
+        const int j = base + t;
+        const bool valid = j < ncr && j < P.nc_max;
+        double c0 = 0, c1 = 0, c2 = 0;
+        if (valid) {
+            const gdouble* c = gptr(P.cir) + ((size_t)b * P.nc_max + j) * 3;
+            c0 = c[0]; c1 = c[1]; c2 = c[2];
+        }
+        const double d = (x0v0 - c0) * (x0v0 - c0) + (x0v1 - c1) * (x0v1 - c1) - c2 * c2;
+        const bool keep = valid && (!P.select_obs || d <= P.detect_r2);
+        const unsigned m = gballot(keep);
+        const int pos = ncs + __builtin_popcount(m & ((1u << t) - 1u));
+        if (keep) {
+            w.obs[3 * pos + 0] = c0;
+            w.obs[3 * pos + 1] = c1;
+            w.obs[3 * pos + 2] = c2;
+        }
+        ncs += __builtin_popcount(m);
+    }
+    for (int base = 0; base < P.ne_max; base += GLANES) {
+        const int j = base + t;
+        const bool valid = j < ner && j < P.ne_max;
+        double e[5] = {0, 0, 0, 0, 0};
+        if (valid) {
+            const gdouble* ep = gptr(P.elp) + ((size_t)b * P.ne_max + j) * 5;
+            for (int i = 0; i < 5; ++i) e[i] = ep[i];
+        }
+        const double rmax = e[2] > e[3] ? e[2] : e[3];
+        const double d = (x0v0 - e[0]) * (x0v0 - e[0]) + (x0v1 - e[1]) * (x0v1 - e[1]) - rmax * rmax;
+        const bool keep = valid && (!P.select_obs || d <= P.detect_r2);
+        const unsigned m = gballot(keep);
+        const int pos = nes + __builtin_popcount(m & ((1u << t) - 1u));
+        if (keep) {
+            double* o = w.obs + 3 * P.nc_max + 5 * pos;
+            for (int i = 0; i < 5; ++i) o[i] = e[i];
+            double ce, se;
+            sincos(e[4], &se, &ce);
+            double* qq = w.obs + 3 * P.nc_max + 5 * P.ne_max;
+            qq[pos] = (e[3] * ce) * (e[3] * ce) + (e[2] * se) * (e[2] * se);
+            qq[P.ne_max + pos] = 2 * ce * se * (e[3] * e[3] - e[2] * e[2]);
+            qq[2 * P.ne_max + pos] = (e[3] * se) * (e[3] * se) + (e[2] * ce) * (e[2] * ce);
+            qq[3 * P.ne_max + pos] = (e[3] * e[2]) * (e[3] * e[2]);
+        }
+        nes += __builtin_popcount(m);
+    }
+    // the instance's u (the rollout below reads it from LDS)
+    for (int j = t; j < nu; j += GLANES) w.uv[j] = gptr(P.u0)[(size_t)b * nu + j];
+    wave_sync();
+    // detour goal (MPC_LIP_modi.py:247-271): first selected circle that triggers
+    double gxg = g0, gyg = g1;
+    bool found = false;
+    for (int base = 0; P.detour && !found && base < ncs; base += GLANES) {
+        const int j = base + t;
+        bool fire = false;
+        double nx = 0, ny = 0;
+        if (j < ncs) {
+            const double* c = w.obs + 3 * j;
+            const double cen = (x0v0 - c[0]) * (x0v0 - c[0]) + (x0v1 - c[1]) * (x0v1 - c[1]);
+            const double gd = (x0v0 - g0) * (x0v0 - g0) + (x0v1 - g1) * (x0v1 - g1);
+            if (cen < gd && cen < 9 * c[2] * c[2]) {
+                const double th = atan2(g1 - x0v1, g0 - x0v0);
+                const double al = atan2(c[1] - x0v1, c[0] - x0v0);
+                double dd = th - al;
+                if (dd < 0 && fabs(dd) > M_PI)
+                    dd += 2 * M_PI;
+                else if (dd > 0 && fabs(dd) > M_PI)
+                    dd -= 2 * M_PI;
+                if (fabs(dd) < M_PI / 12) {
+                    fire = true;
+                    const double na = dd < 0 ? th - M_PI / 12 : th + M_PI / 12;
+                    const double rr = sqrt(gd);
+                    double sn, cs;
+                    sincos(na, &sn, &cs);
+                    nx = x0v0 + rr * cs;
+                    ny = x0v1 + rr * sn;
+                }
+            }
+        }
+        const unsigned m = gballot(fire);
+        if (m) {
+            const int first = __builtin_ctz(m);
+            gxg = __shfl(nx, first, GLANES);
+            gyg = __shfl(ny, first, GLANES);
+            found = true;
+        }
+    }
+    // V = E x0 + G u (the reference's rollout of u)
+    double xb[5];
+#pragma unroll
+    for (int c = 0; c < 5; ++c) xb[c] = x0[c];
+    for (int g = t; g < NG; g += GLANES) {
+        double v = 0.0;
+#pragma unroll
+        for (int c = 0; c < 5; ++c) v += E[g * 5 + c] * xb[c];
+        const double* gr = G + g * NCP;
+#pragma unroll
+        for (int j = 0; j < nu; ++j) v += gr[j] * w.uv[j];
+        w.V[g] = v;
+        w.gfg[g] = 0.0;
+    }
+    wave_sync();
+    // state pass: lanes 1..N own x_k (cos/sin of theta_k, the objective term f_k and its gradient)
+    double fk = 0.0;
+    if (t >= 1 && t <= N) {
+        const int k = t;
+        const double th = w.V[gx(k, 4)];
+        double s_, c_;
+        lsincos(th, &s_, &c_);
+        w.CT[k] = c_;
+        w.ST[k] = s_;
+        const double px = w.V[gx(k, 0)], py = w.V[gx(k, 1)];
+        const double wk = P.q + (k == 1 ? P.p : 0.0);
+        const double ex = px - gxg, ey = py - gyg;
+        const double dxg = gxg - px, dyg = gyg - py;
+        const double phi = th - latan2(dyg, dxg);
+        fk = wk * (ex * ex + ey * ey) + P.r * phi * phi;
+        const double rho2 = dxg * dxg + dyg * dyg;
+        w.gfg[gx(k, 0)] = 2 * wk * ex + 2 * P.r * phi * (-dyg / rho2);
+        w.gfg[gx(k, 1)] = 2 * wk * ey + 2 * P.r * phi * (dxg / rho2);
+        w.gfg[gx(k, 4)] = 2 * P.r * phi;
+    }
+    const double f = gsum16(fk);
+    wave_sync();
+    // rows: values, bounds, activity, generator-form Jacobian rows
+    const size_t mm = (size_t)P.m_max;
+    for (int r = t; r < P.mr4; r += GLANES) {
+        const RowInfo ri = decode_row(P, r, ncs, nes);
+        double cf[4];
+        int gn[4];
+        const double c = row_eval<N, true>(P, ri, w.V, w.CT, w.ST, w.obs, 0.0, cf, gn);
+        st4(w.rcoef + 4 * r, cf[0], cf[1], cf[2], cf[3]);
+        *reinterpret_cast<uint32_t*>(w.rgen + 4 * r) =
+            (uint32_t)gn[0] | ((uint32_t)gn[1] << 8) | ((uint32_t)gn[2] << 16) | ((uint32_t)gn[3] << 24);
+        if (r < P.m_max) {
+            double clv, cuv;
+            row_bounds(P, ri, legv, clv, cuv);
+            if (P.c_out) gptr(P.c_out)[b * mm + r] = c;
+            if (P.cl_out) gptr(P.cl_out)[b * mm + r] = clv;
+            if (P.cu_out) gptr(P.cu_out)[b * mm + r] = cuv;
+            if (P.active_out) gptr(P.active_out)[b * mm + r] = ri.type != R_NONE;
+        }
+    }
+    wave_sync();
+    // J rows (dense, u-space): lane t writes columns t (+ 16)
+    if (P.J_out) {
+        gdouble* Jb = gptr(P.J_out + (size_t)b * mm * nu);
+        // 4 rows per step (mr4 is a multiple of 4): every LDS read of the step is issued before the FMAs
+        for (int r0 = 0; r0 < P.m_max; r0 += 4) {
+            const uint4 pk4 = *reinterpret_cast<const uint4*>(w.rgen + 4 * r0);
+            const uint32_t pk[4] = {pk4.x, pk4.y, pk4.z, pk4.w};
+            double cf[4][4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) ld4(w.rcoef + 4 * (r0 + i), cf[i][0], cf[i][1], cf[i][2], cf[i][3]);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int r = r0 + i;
+#pragma unroll
+                for (int T = 0; T < NTU; ++T) {
+                    const int j = GLANES * T + t;
+                    const double v = cf[i][0] * G[gen_i(pk[i], 0) * NCP + j] + cf[i][1] * G[gen_i(pk[i], 1) * NCP + j] +
+                                     cf[i][2] * G[gen_i(pk[i], 2) * NCP + j] + cf[i][3] * G[gen_i(pk[i], 3) * NCP + j];
+                    if (j < nu && r < P.m_max) Jb[(size_t)r * nu + j] = v;
+                }
+            }
+        }
+    }
+    // grad f = G^T (d f / d V) (x_0 and the p_k generators carry no objective gradient)
+    if (P.grad_out) {
+#pragma unroll
+        for (int T = 0; T < NTU; ++T) {
+            const int j = GLANES * T + t;
+            double gf = 0.0;
+            for (int g = 8; g < NG; ++g) gf += G[g * NCP + j] * w.gfg[g];
+            if (j < nu) gptr(P.grad_out)[b * nu + j] = gf;
+        }
+    }
+    if (t == 0) {
+        if (P.f_out) gptr(P.f_out)[b] = f;
+        if (P.goal_eff_out) {
+            gptr(P.goal_eff_out)[2 * b] = gxg;
+            gptr(P.goal_eff_out)[2 * b + 1] = gyg;
+        }
+    }
+    wave_sync();
+}
+
+template <int N>
+__global__ __launch_bounds__(256) void eval_kernel(KP Pv)
+{
+    using D = Dim<N>;
     constexpr int NCP = D::NCPU;
     constexpr int NG = D::NG;
-    constexpr int RPL = 2;
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    // kernel parameters live in LDS: keeps ~90 kernarg SGPRs from being pinned across the solve
+    // kernel parameters live in LDS: keeps ~90 kernarg SGPRs from being pinned across the sweep
     KP* Ps = reinterpret_cast<KP*>(smem);
     double* G = smem + KP_DOUBLES;
     double* E = G + NG * NCP;
@@ -1978,78 +2124,13 @@ __global__ __launch_bounds__(256, 4) void eval_kernel(KP Pv)
     for (int i = threadIdx.x; i < NG * 5; i += blockDim.x) E[i] = Pv.E[i];
     __syncthreads();
     const KP& P = *Ps;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);   // wave-uniform (SGPR)
-    const int lane = lane_id();
-    WS<N> w = carve<N>(wsb + (size_t)wv * ws_doubles<N>(P.nc_max, P.ne_max, P.mr4), P.nc_max, P.ne_max, P.mr4);
-    // grid-stride over instances: the G/E staging above is paid once per workgroup, not per instance
-    for (long long b = (long long)blockIdx.x * WAVES_PER_BLOCK + wv; b < P.B;
-         b += (long long)gridDim.x * WAVES_PER_BLOCK) {
-    double gxg, gyg, uj;
-    int legv;
-    prologue<N, true>(P, w, G, E, b, gxg, gyg, legv, uj);
-    const int nc_sel = w.nsel[0], ne_sel = w.nsel[1];
-    const double fk = state_pass<N, true>(P, w.V, w.CT, w.ST, w.gfg, gxg, gyg);
-    const double f = wsum(fk);
-    wave_sync();
-    const size_t mm = (size_t)P.m_max;
-#pragma unroll
-    for (int q = 0; q < RPL; ++q) {
-        const int r = lane + WAVE * q;
-        if (r < P.mr4) {
-            const RowInfo ri = decode_row(P, r, nc_sel, ne_sel);
-            double cf[4];
-            int gn[4];
-            const double c = row_eval<N, true>(P, ri, w.V, w.CT, w.ST, w.obs, 0.0, cf, gn);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                w.rcoef[4 * r + i] = cf[i];
-                w.rgen[4 * r + i] = (uint8_t)gn[i];
-            }
-            if (r < P.m_max) {
-                double clv, cuv;
-                row_bounds(P, ri, legv, clv, cuv);
-                if (P.c_out) P.c_out[b * mm + r] = c;
-                if (P.cl_out) P.cl_out[b * mm + r] = clv;
-                if (P.cu_out) P.cu_out[b * mm + r] = cuv;
-                if (P.active_out) P.active_out[b * mm + r] = ri.type != R_NONE;
-            }
-        }
-    }
-    wave_sync();
-    const int g4 = lane >> 4, col = lane & 15;
-    if (P.J_out) {
-        for (int s4 = 0; s4 < P.mr4; s4 += 4) {
-            const int r = s4 + g4;
-            if (r < P.m_max) {
-#pragma unroll
-                for (int T = 0; T < NT; ++T) {
-                    const int j = 16 * T + col;
-                    if (j < n) P.J_out[(b * mm + r) * n + j] = jrow_col(w.rcoef, w.rgen, G, NCP, r, j);
-                }
-            }
-        }
-    }
-    double gfc[NT];
-#pragma unroll
-    for (int T = 0; T < NT; ++T) gfc[T] = 0.0;
-    for (int t = 4 + g4; t < NG; t += 4) {
-        const double gv = w.gfg[t];
-#pragma unroll
-        for (int T = 0; T < NT; ++T) gfc[T] += G[t * NCP + 16 * T + col] * gv;
-    }
-#pragma unroll
-    for (int T = 0; T < NT; ++T) {
-        gfc[T] = gsum(gfc[T]);
-        if (P.grad_out && g4 == 0 && 16 * T + col < n) P.grad_out[b * n + 16 * T + col] = gfc[T];
-    }
-    if (lane == 0) {
-        if (P.f_out) P.f_out[b] = f;
-        if (P.goal_eff_out) {
-            P.goal_eff_out[2 * b] = gxg;
-            P.goal_eff_out[2 * b + 1] = gyg;
-        }
-    }
-    wave_sync();
+    const int gi = threadIdx.x / GLANES, t = threadIdx.x & (GLANES - 1);
+    const GWS<N> w = carve_g<N>(wsb + (size_t)gi * gws_doubles<N>(P.nc_max, P.ne_max, P.mr4), P.nc_max, P.ne_max, P.mr4);
+    // grid-stride over instances (the G/E staging above is paid once per workgroup); the 4 groups of a wave
+    // take 4 consecutive instances
+    for (long long b0 = (long long)blockIdx.x * GROUPS_PER_BLOCK; b0 < P.B; b0 += (long long)gridDim.x * GROUPS_PER_BLOCK) {
+        const long long b = b0 + gi;
+        if (b < P.B) eval_group_one<N>(P, w, G, E, b, t);
     }
 }
 
@@ -3422,7 +3503,11 @@ void launch_solve(const KP& P0, size_t smem, hipStream_t st, unsigned* res_out)
             return;
         }
         // a persistent grid of at most the resident workgroups (the work queue hands out the instances)
-        const unsigned grid = res > 0 && res < need ? res : need;
+        unsigned grid = res > 0 && res < need ? res : need;
+#ifdef ALIP_DEV_GRID
+        static const unsigned cap = (unsigned)atoi(getenv("ALIP_GRID") ? getenv("ALIP_GRID") : "0");
+        if (cap > 0 && grid > cap) grid = cap;
+#endif
         hipLaunchKernelGGL(kern, dim3(grid), dim3(WAVE * WAVES_PER_BLOCK), smem, st, P0);
     };
     if (P0.mo4 <= 32)
@@ -3445,15 +3530,16 @@ void launch_solve(const KP& P0, size_t smem, hipStream_t st, unsigned* res_out)
 template <int N>
 hipError_t launch_t(bool solve, bool f32, const KP& P, size_t smem, hipStream_t st, unsigned* res_out)
 {
-    const unsigned grid = (unsigned)((P.B + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
     if (solve && f32) {
         launch_solve<N, float>(P, smem, st, res_out);
     } else if (solve) {
         launch_solve<N, double>(P, smem, st, res_out);
     } else {
-        // grid-stride eval kernel: at most 8 workgroups per CU resident at once on the 256 CUs
-        const unsigned egrid = grid < 2048u ? grid : 2048u;
+        // grid-stride eval kernel (16 instances per workgroup): at most the resident workgroups
         set_smem((const void*)eval_kernel<N>, smem);
+        const unsigned need = (unsigned)((P.B + GROUPS_PER_BLOCK - 1) / GROUPS_PER_BLOCK);
+        const unsigned res = resident_blocks((const void*)eval_kernel<N>, smem);
+        const unsigned egrid = res > 0 && res < need ? res : (need > 0 ? need : 1u);
         hipLaunchKernelGGL(eval_kernel<N>, dim3(egrid), dim3(WAVE * WAVES_PER_BLOCK), smem, st, P);
     }
     return hipGetLastError();
@@ -3781,7 +3867,7 @@ size_t smem_bytes(const Handle* h, bool solve)
     case NN:                                                                                           \
         wsd = solve ? (f32 ? wss_elems<NN, float>(h->cfg.nc_max, h->cfg.ne_max, h->mr4_s, h->mo4)      \
                            : wss_elems<NN, double>(h->cfg.nc_max, h->cfg.ne_max, h->mr4_s, h->mo4)) \
-                    : ws_doubles<NN>(h->cfg.nc_max, h->cfg.ne_max, h->mr4);                            \
+                    : gws_doubles<NN>(h->cfg.nc_max, h->cfg.ne_max, h->mr4);                           \
         break;
         WSCASE(1) WSCASE(2) WSCASE(3) WSCASE(4) WSCASE(5) WSCASE(6)
 #undef WSCASE
@@ -3789,8 +3875,9 @@ size_t smem_bytes(const Handle* h, bool solve)
     const int e = solve ? ((h->NG * 5 + 3) & ~3) : h->NG * 5 + ((h->NG * 5) & 1);
     const int ncp = solve ? h->NCP : h->NCPU;
     // KP in fp64 units, then G, E and the per-wave workspaces in the kernel's arithmetic type
+    const size_t per_block = solve ? (size_t)WAVES_PER_BLOCK : (size_t)GROUPS_PER_BLOCK;   // workspaces
     return sizeof(double) * (size_t)KP_DOUBLES +
-           (f32 ? sizeof(float) : sizeof(double)) * ((size_t)h->NG * ncp + e + (size_t)WAVES_PER_BLOCK * wsd);
+           (f32 ? sizeof(float) : sizeof(double)) * ((size_t)h->NG * ncp + e + per_block * wsd);
 }
 
 KP make_kp(const Handle* h, long long B, bool solve)

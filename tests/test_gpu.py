@@ -857,3 +857,33 @@ def test_closed_loop_matches_oracle(gpu_lib, coracle, variant, kick, program):
     done = o["status"] == gpu_lib.ROLLOUT_DONE
     for b in np.nonzero(o["steps_to_goal"] > 0)[0]:
         assert done[b, o["steps_to_goal"][b]:].all() and not done[b, :o["steps_to_goal"][b]].any()
+
+
+@pytest.mark.parametrize("N,nc,ne,variant", [(3, 5, 0, 0), (3, 5, 0, 1), (6, 5, 5, 0), (2, 20, 0, 0), (1, 4, 20, 1)])
+def test_eval_batch_vs_oracle(gpu_lib, coracle, N, nc, ne, variant):
+    """The Jacobian sweep (eval_kernel, 16 lanes per instance, grid-stride) on a ragged batch of seeded random
+    scenes against the C oracle's reference callbacks (select_obs and detour on): every output of every
+    instance, including > 16 obstacle slots (select_obs / detour in two 16-slot passes)."""
+    from alipmpc import scenes
+    B = 5003
+    bt = scenes.make_batch_vec(B, seed=17 + N, n_cir=nc, n_elp=ne, N=N)
+    # the generator mixes part of the circles into ellipses: trim / pad (shifted copies) to exactly nc, ne slots
+    for key, cnt, want, d in (("cir", "nc", nc, 3), ("elp", "ne", ne, 5)):
+        if want == 0:
+            continue
+        a = bt[key][:, :want]
+        while a.shape[1] < want:
+            extra = min(a.shape[1], want - a.shape[1])
+            a = np.concatenate([a, a[:, :extra] + np.r_[0.7, -0.6, np.zeros(d - 2)]], axis=1)
+        bt[key] = np.ascontiguousarray(a)
+        bt[cnt] = np.clip(bt[cnt] + want, 0, want).astype(np.int32)
+    s = gpu_lib.Solver(gpu_lib.default_cfg(variant, N, nc_max=nc, ne_max=ne))
+    u = bt["u0"] + 0.05 * np.random.default_rng(3).standard_normal(bt["u0"].shape)
+    o = s.eval(bt["x0"], bt["goal"], bt["leg"], bt["cir"], bt["nc"], bt.get("elp"), bt.get("ne"), u)
+    r = coracle.eval_batch(coracle.default_cfg(variant, N, nc_max=nc, ne_max=ne), bt["x0"], bt["goal"], bt["leg"],
+                           bt["cir"], bt["nc"], bt.get("elp"), bt.get("ne"), u)
+    assert rel(o["f"], r["f"]) < 1e-11
+    assert rel(o["grad"], r["grad"]) < 1e-11
+    assert np.array_equal(o["row_active"], r["row_active"])
+    assert rel(o["c"], r["c"]) < 1e-11 and rel(o["J"], r["J"]) < 1e-11
+    assert np.array_equal(o["cl"], r["cl"]) and np.array_equal(o["cu"], r["cu"])

@@ -1,0 +1,39 @@
+"""Dev: Jacobian-sweep time with / without its outputs, and the box's plain fill / copy bandwidth."""
+import os, sys, numpy as np, torch
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "mujoco-lip-mpc-simulation_amd"))
+import alipmpc
+from alipmpc import scenes
+dev = torch.device("cuda", 0)
+Bs = 65536
+cfg = alipmpc.default_cfg(0, 3, nc_max=5, ne_max=0)
+s = alipmpc.Solver(cfg)
+bt = scenes.make_batch_vec(Bs, seed=7, n_cir=5, N=3, fields=4096)
+n, m = 15, 3 * s.rps
+inp = {"x0": torch.from_numpy(bt["x0"]).to(dev), "goal": torch.from_numpy(bt["goal"]).to(dev),
+       "leg": torch.from_numpy(bt["leg"].astype(np.int8)).to(dev), "cir": torch.from_numpy(bt["cir"]).to(dev),
+       "nc": torch.from_numpy(bt["nc"].astype(np.int32)).to(dev), "u": torch.from_numpy(bt["u0"]).to(dev)}
+full = {"f": torch.empty(Bs, dtype=torch.float64, device=dev), "grad": torch.empty((Bs, n), dtype=torch.float64, device=dev),
+        "c": torch.empty((Bs, m), dtype=torch.float64, device=dev), "J": torch.empty((Bs, m, n), dtype=torch.float64, device=dev)}
+st = torch.cuda.current_stream()
+def t(out, reps=8):
+    for _ in range(2): s.eval_device(inp, out, stream=st)
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for a, b in ev:
+        a.record(st); s.eval_device(inp, out, stream=st); b.record(st)
+    torch.cuda.synchronize()
+    return float(np.median([a.elapsed_time(b) for a, b in ev]))
+print("full      ", t(full))
+print("no J      ", t({k: v for k, v in full.items() if k != "J"}))
+print("f only    ", t({"f": full["f"]}))
+x = torch.empty(Bs * 4272 // 8, dtype=torch.float64, device=dev)
+y = torch.empty_like(x)
+for name, fn in (("fill", lambda: x.fill_(1.0)), ("copy", lambda: y.copy_(x))):
+    for _ in range(3): fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(); [fn() for _ in range(10)]; b.record(); torch.cuda.synchronize()
+    ms = a.elapsed_time(b) / 10
+    nb = x.numel() * 8 * (1 if name == "fill" else 2)
+    print(f"{name} {nb/1e6:.0f} MB {ms:.4f} ms {nb/ms/1e6:.0f} GB/s")

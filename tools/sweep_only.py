@@ -1,18 +1,16 @@
-"""Dev: time only the Jacobian sweep (eval_kernel, bench.jacobian_sweep) — the program for rocprofv3
-kernel-trace / PMC passes of that kernel.   python tools/sweep_only.py [B] [reps]"""
-import json
-import os
-import sys
-import types
-
+"""Dev: the bench's Jacobian sweep alone (eval_kernel on 65536 cfg2-shaped instances), for rocprofv3 passes."""
+import os, sys
+import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-import bench  # noqa: E402  (puts the package on sys.path)
-import torch  # noqa: E402
-import alipmpc  # noqa: E402
-from alipmpc import scenes  # noqa: E402
+import torch
+import bench
 
-B = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
-reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
-args = types.SimpleNamespace(sweep_batch=B, seed=0)
-print(json.dumps(bench.jacobian_sweep(alipmpc, scenes, 0, args, torch.device("cuda", 0), reps=reps)))
+class A:
+    sweep_batch = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+    seed = 0
+sys.path.insert(0, os.path.join(ROOT, "mujoco-lip-mpc-simulation_amd"))
+import alipmpc
+from alipmpc import scenes
+r = bench.jacobian_sweep(alipmpc, scenes, alipmpc.VARIANT_MODI, A, torch.device("cuda", 0), reps=6)
+print(r)
