@@ -177,16 +177,18 @@ def main():
     peak = FP32_PEAK_TFLOPS if (fp32 and program == "wave") else FP64_PEAK_TFLOPS
     launch_flops = fpi * float(iters.sum())
     achieved = launch_flops / (kernel_ms * 1e-3) / 1e12
-    traffic = None
-    tp = os.path.join(ROOT, "profiles", "solve_kernel_traffic.json")
+    # counter-derived fields of the dominant kernel from the committed rocprofv3 passes of this config
+    # (tools/roofline.py writes profiles/solve_kernel_counters.json from profiles/r2/<config>/): HBM traffic and
+    # the issue / MFMA shares that say which bound the kernel actually sits against
+    prof = {}
+    tp = os.path.join(ROOT, "profiles", "solve_kernel_counters.json")
     if os.path.exists(tp):
         try:
             with open(tp) as fh:
-                tj = json.load(fh)
-            if tj.get("B") == B and tj.get("N") == N and not fp32 and not n_elp and tj.get("kernel", kname) == kname:
-                traffic = tj.get("hbm_bytes_per_launch")
+                prof = json.load(fh).get(f"{kname}|B={B}", {})
         except Exception:
-            traffic = None
+            prof = {}
+    traffic = prof.get("hbm_bytes_per_launch")
 
     # quality beside the rate (every config): solves/s counts every instance, so report how many of them
     # converged and how many returned plans are feasible for the reference constraints
@@ -238,6 +240,11 @@ def main():
                 "unit": "TFLOP/s",
                 "frac": achieved / peak,
                 "traffic": traffic,
+                "valu_issue_frac": prof.get("valu_issue_frac"),
+                "active_issue_frac": prof.get("active_issue_frac"),
+                "mfma_busy_share": prof.get("mfma_busy_share"),
+                "insts_per_iter": prof.get("insts_per_iter"),
+                "counters": "profiles/solve_kernel_counters.json (tools/roofline.py)" if prof else None,
                 "kernel_ms": kernel_ms,
                 "flops_per_iter": fpi,
                 "iters_per_launch": int(iters.sum()),

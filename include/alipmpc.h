@@ -230,6 +230,16 @@ int alipmpc_closed_loop_batch(void* handle, int64_t B, int32_t S, int32_t f_cyc,
                               double* foot_traj, double* x_traj, double* hd_traj, int32_t* status_traj,
                               int32_t* iters_traj, int32_t* steps_to_goal, void* hip_stream);
 
+/* Nominal gait of a batch (replaces MPCCBF.alip_des_vel / cal_foot_with_veldes, MPC_LIP_modi.py:181-194, used by
+ * the driver at main_sim_mpc.py:54 and the ALIP-only loggers):
+ *   vel_des = alip_des_vel(vx_max, leg_ind) = [sigma vx_max T / 2, 0.5 (-0.5 leg_ind step_gap) beta sinh(beta T) /
+ *             (cosh(beta T) + 1)], sigma = beta coth(beta T / 2), step_gap = 0.3 — or the given vel_des_in (B x 2),
+ *   foot    = cal_foot_with_veldes(x, vel_des) = B_vel^-1 (vel_des - (A x)[2:4]), B_vel = B[2:4, 0:2].
+ * x B x 5 states, leg B leg_ind (ignored when vel_des_in is given), vel_des B x 2 (may be NULL), foot B x 2.
+ * Host pointers with hip_stream = NULL (synchronous), device pointers otherwise. */
+int alipmpc_nominal_gait_batch(void* handle, int64_t B, double vx_max, const double* x, const int8_t* leg,
+                               const double* vel_des_in, double* vel_des, double* foot, void* hip_stream);
+
 /* Rows per planned step of alipmpc_trace_batch: 1 + len(np.arange(0, dt + 0.01, 0.01)) (42 at dt = 0.4);
  * 0 for the DD variant. */
 int32_t alipmpc_trace_len(const alipmpc_cfg* cfg);

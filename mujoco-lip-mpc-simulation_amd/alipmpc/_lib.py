@@ -40,7 +40,7 @@ class Cfg(ctypes.Structure):
 EXPORTS = ("alipmpc_default_cfg", "alipmpc_rows_per_step", "alipmpc_num_vars", "alipmpc_create",
            "alipmpc_solve_batch", "alipmpc_eval_batch", "alipmpc_rollout_batch", "alipmpc_closed_loop_batch",
            "alipmpc_trace_len",
-           "alipmpc_trace_batch", "alipmpc_solve_slots", "alipmpc_solve_program", "alipmpc_last_kernel_ms",
+           "alipmpc_trace_batch", "alipmpc_nominal_gait_batch", "alipmpc_solve_slots", "alipmpc_solve_program", "alipmpc_last_kernel_ms",
            "alipmpc_last_error", "alipmpc_destroy")
 
 _lib = None
@@ -85,6 +85,9 @@ def load(build_if_missing=True):
     L.alipmpc_trace_len.restype = ctypes.c_int32
     L.alipmpc_trace_batch.argtypes = [P, ctypes.c_int64, P, P, P, P]
     L.alipmpc_trace_batch.restype = ctypes.c_int
+    if hasattr(L, "alipmpc_nominal_gait_batch"):   # (absent from older dev builds used for A/B timing)
+        L.alipmpc_nominal_gait_batch.argtypes = [P, ctypes.c_int64, ctypes.c_double, P, P, P, P, P, P]
+        L.alipmpc_nominal_gait_batch.restype = ctypes.c_int
     if hasattr(L, "alipmpc_solve_slots"):     # (absent from older dev builds used for A/B timing)
         L.alipmpc_solve_slots.argtypes = [P, ctypes.POINTER(ctypes.c_int64)]
         L.alipmpc_solve_slots.restype = ctypes.c_int
@@ -297,6 +300,19 @@ class Solver:
             _ptr(inp.get("ne")), _ptr(out.get("foot")), _ptr(out.get("x")), _ptr(out.get("hd")),
             _ptr(out.get("status")), _ptr(out.get("iters")), _ptr(out.get("steps_to_goal")), _stream_arg(st))
         self._check(rc, "alipmpc_closed_loop_batch")
+
+    def nominal_gait(self, x, leg=None, vx_max=0.6, vel_des=None):
+        """Nominal gait (alipmpc_nominal_gait_batch): returns (vel_des (B,2), foot (B,2)) — alip_des_vel(vx_max,
+        leg_ind) per instance (or the given vel_des) and cal_foot_with_veldes(x, vel_des)."""
+        x = np.ascontiguousarray(x, np.float64).reshape(-1, 5)
+        B = x.shape[0]
+        lg = None if leg is None else np.ascontiguousarray(np.broadcast_to(np.asarray(leg), (B,)), np.int8)
+        vin = None if vel_des is None else np.ascontiguousarray(np.broadcast_to(vel_des, (B, 2)), np.float64)
+        vout, foot = np.zeros((B, 2)), np.zeros((B, 2))
+        rc = self._L.alipmpc_nominal_gait_batch(self._h, B, float(vx_max), _ptr(x), _ptr(lg), _ptr(vin), _ptr(vout),
+                                                _ptr(foot), None)
+        self._check(rc, "alipmpc_nominal_gait_batch")
+        return vout, foot
 
     def trace(self, x0, u):
         """Dense plan traces (alipmpc_trace_batch): x0 (B,5), u (B,5N) -> (B, N, trace_len, 2)."""

@@ -3397,6 +3397,40 @@ __global__ __launch_bounds__(256) void cl_init_kernel(CLP C)
 // (1 - ch) p_k[0:2].  x_{k+1} = M_A x_k + M_B u_k and p_k = W (u_k - A x_k) as gen_control_test forms them.
 // One thread per output row (coalesced 16-byte stores); HBM-bound: 40 B of plan in, rows x 16 B out.
 // ------------------------------------------------------------------------------------------------
+// nominal gait (MPC_LIP_modi.py:181-194): vel_des = alip_des_vel(vx_max, leg_ind) unless a target velocity is
+// given, foot = cal_foot_with_veldes(x, vel_des) = B_vel^-1 (vel_des - (A x)[2:4]) with B_vel = -beta sinh(beta T) I
+struct NgP {
+    long long B;
+    double vdx, vdy0;     // sigma vx_max T / 2 and -0.25 step_gap beta sinh(beta T) / (cosh(beta T) + 1) per unit leg_ind
+    double bsh, ch, ibv;  // beta sinh(beta T), cosh(beta T), 1 / (-beta sinh(beta T))
+    const double* x;
+    const int8_t* leg;
+    const double* vin;
+    double* vout;
+    double* foot;
+};
+__global__ __launch_bounds__(256) void nominal_gait_kernel(NgP Q)
+{
+    const long long b = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= Q.B) return;
+    const double* x = Q.x + 5 * b;
+    double v0, v1;
+    if (Q.vin) {
+        v0 = Q.vin[2 * b];
+        v1 = Q.vin[2 * b + 1];
+    } else {
+        v0 = Q.vdx;
+        v1 = 0.5 * (-0.5 * (double)Q.leg[b] * 0.3) * Q.vdy0;
+    }
+    if (Q.vout) {
+        Q.vout[2 * b] = v0;
+        Q.vout[2 * b + 1] = v1;
+    }
+    const double ax = Q.bsh * x[0] + Q.ch * x[2], ay = Q.bsh * x[1] + Q.ch * x[3];
+    Q.foot[2 * b] = Q.ibv * (v0 - ax);
+    Q.foot[2 * b + 1] = Q.ibv * (v1 - ay);
+}
+
 struct TrP {
     long long B;
     int N, rows;        // rows per step = 1 + samples
@@ -4640,6 +4674,58 @@ int alipmpc_trace_batch(void* handle, int64_t B, const double* x0, const double*
     HIPCHK(h, hipGetLastError());
     if (host) {
         HIPCHK(h, hipMemcpyAsync(trace, T.trace, nout * 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(h, hipStreamSynchronize(st));
+    }
+    return ALIPMPC_OK;
+}
+
+int alipmpc_nominal_gait_batch(void* handle, int64_t B, double vx_max, const double* x, const int8_t* leg,
+                               const double* vel_des_in, double* vel_des, double* foot, void* hip_stream)
+{
+    Handle* h = (Handle*)handle;
+    if (!h) return ALIPMPC_EINVAL;
+    const alipmpc_cfg& cf = h->cfg;
+    if (cf.variant == ALIPMPC_VARIANT_DD) return fail(h, ALIPMPC_EUNSUPPORTED, "nominal gait: LIP variants only");
+    if (B < 0) return fail(h, ALIPMPC_EINVAL, "B < 0");
+    if (B == 0) return ALIPMPC_OK;
+    if (!x || !foot || (!leg && !vel_des_in)) return fail(h, ALIPMPC_EINVAL, "missing pointer");
+    HIPCHK(h, hipSetDevice(h->device));
+    const size_t Bz = (size_t)B;
+    NgP Q;
+    std::memset(&Q, 0, sizeof(Q));
+    Q.B = B;
+    {
+        const double b = std::sqrt(cf.g / cf.H), T = cf.dt, sh = std::sinh(b * T), ch = std::cosh(b * T);
+        const double sigma = b / std::tanh(T * b / 2);   // beta coth(beta T / 2)
+        Q.vdx = sigma * vx_max * T / 2;
+        Q.vdy0 = (b * sh) / (ch + 1);
+        Q.bsh = sh * b;
+        Q.ch = ch;
+        Q.ibv = 1.0 / (-sh * b);
+    }
+    hipStream_t st = stream_of(h, hip_stream);
+    const bool host = hip_stream == nullptr;
+    if (host) {
+        if (int rc = ensure_stage(h, Bz * 8 * (5 + 2 + 2 + 2) + Bz + 5 * 256)) return rc;   // 5 carves, 256 B aligned
+        Carver cv{(char*)h->stage};
+        double* dx = cv.take<double>(Bz * 5);
+        double* dvi = cv.take<double>(Bz * 2);
+        double* dvo = cv.take<double>(Bz * 2);
+        double* df = cv.take<double>(Bz * 2);
+        int8_t* dl = cv.take<int8_t>(Bz);
+        HIPCHK(h, hipMemcpyAsync(dx, x, Bz * 5 * 8, hipMemcpyHostToDevice, st));
+        if (vel_des_in) HIPCHK(h, hipMemcpyAsync(dvi, vel_des_in, Bz * 2 * 8, hipMemcpyHostToDevice, st));
+        if (leg) HIPCHK(h, hipMemcpyAsync(dl, leg, Bz, hipMemcpyHostToDevice, st));
+        Q.x = dx; Q.vin = vel_des_in ? dvi : nullptr; Q.leg = leg ? dl : nullptr;
+        Q.vout = vel_des ? dvo : nullptr; Q.foot = df;
+    } else {
+        Q.x = x; Q.vin = vel_des_in; Q.leg = leg; Q.vout = vel_des; Q.foot = foot;
+    }
+    hipLaunchKernelGGL(nominal_gait_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, st, Q);
+    HIPCHK(h, hipGetLastError());
+    if (host) {
+        if (vel_des) HIPCHK(h, hipMemcpyAsync(vel_des, Q.vout, Bz * 2 * 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(h, hipMemcpyAsync(foot, Q.foot, Bz * 2 * 8, hipMemcpyDeviceToHost, st));
         HIPCHK(h, hipStreamSynchronize(st));
     }
     return ALIPMPC_OK;

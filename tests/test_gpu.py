@@ -887,3 +887,37 @@ def test_eval_batch_vs_oracle(gpu_lib, coracle, N, nc, ne, variant):
     assert np.array_equal(o["row_active"], r["row_active"])
     assert rel(o["c"], r["c"]) < 1e-11 and rel(o["J"], r["J"]) < 1e-11
     assert np.array_equal(o["cl"], r["cl"]) and np.array_equal(o["cu"], r["cu"])
+
+
+def test_nominal_gait_matches_reference_helpers(gpu_lib):
+    """alipmpc_nominal_gait_batch against the planner's restatement of alip_des_vel / cal_foot_with_veldes
+    (MPC_LIP_modi.py:181-194; pinned to the reference by tests/test_oracle.py's g4 goldens): both legs, a given
+    target velocity, host and device pointers."""
+    import torch
+    from alipmpc import planner as pl
+    rng = np.random.default_rng(11)
+    B = 1000
+    x = rng.normal(size=(B, 5)) * np.array([3.0, 3.0, 0.5, 0.5, 1.0])
+    leg = np.where(rng.random(B) < 0.5, -1, 1).astype(np.int8)
+    mp = pl.MPCCBF([[10, 10]], [], [], [], [], [-0.5, 10.5])
+    s = gpu_lib.Solver(gpu_lib.default_cfg(0))
+    vd, foot = s.nominal_gait(x, leg, vx_max=0.6)
+    for b in range(0, B, 7):
+        v_ref = mp.alip_des_vel(0.6, int(leg[b]))
+        np.testing.assert_allclose(vd[b], v_ref, rtol=1e-13, atol=1e-15)
+        np.testing.assert_allclose(foot[b], mp.cal_foot_with_veldes(x[b], v_ref), rtol=1e-12, atol=1e-12)
+    tgt = rng.normal(size=(B, 2)) * 0.3
+    vd2, foot2 = s.nominal_gait(x, vel_des=tgt)
+    assert np.array_equal(vd2, tgt)
+    for b in range(0, B, 11):
+        np.testing.assert_allclose(foot2[b], mp.cal_foot_with_veldes(x[b], tgt[b]), rtol=1e-12, atol=1e-12)
+    # device pointers on the current stream give the same bits
+    dev = torch.device("cuda", 0)
+    xt, lt = torch.from_numpy(x).to(dev), torch.from_numpy(leg).to(dev)
+    vt, ft = torch.empty((B, 2), dtype=torch.float64, device=dev), torch.empty((B, 2), dtype=torch.float64, device=dev)
+    from alipmpc._lib import _ptr
+    rc = s._L.alipmpc_nominal_gait_batch(s._h, B, 0.6, _ptr(xt), _ptr(lt), None, _ptr(vt), _ptr(ft),
+                                         gpu_lib._lib._stream_arg(torch.cuda.current_stream()))
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(ft.cpu().numpy(), foot) and np.array_equal(vt.cpu().numpy(), vd)

@@ -27,13 +27,21 @@ for what in "$@"; do
       python -c "import json;d=json.load(open('$OUT/bench_$c.json'));print('$c', round(d['value']), d['ms_per_step'], d['config']['mean_iters'], d.get('feasible'))"
     done ;;
   prof)
+    # per config: the bench line, a kernel trace and one rocprofv3 pass per counter group (tools/roofline.py)
     cd /tmp
-    echo "=== rocprofv3 kernel trace"
-    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_kt -o kt -- python3 $R/bench.py --steps 10 --no-cpu-baseline > $OUT/prof_kt.log 2>&1 || { tail -20 $OUT/prof_kt.log; exit 1; }
-    for pmc in FETCH_SIZE WRITE_SIZE "SQ_INSTS SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES" "SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
-      tag=$(echo $pmc | cut -d' ' -f1)
-      echo "=== rocprofv3 --pmc $pmc"
-      timeout -s KILL 120 rocprofv3 --pmc $pmc --output-format csv -d $OUT/pmc_$tag -o pmc -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --sweep-batch 0 > $OUT/pmc_$tag.log 2>&1 || { tail -20 $OUT/pmc_$tag.log; exit 1; }
+    for c in ${PROF_CONFIGS:-cfg2 cfg3}; do
+      D=$OUT/$c
+      mkdir -p $D
+      flags="--config $c --no-cpu-baseline --closed-loop-steps 0 --sweep-batch 0"
+      echo "=== bench $c"
+      timeout -k 10 200 python3 $R/bench.py $flags --steps 10 > $D/bench.json 2> $D/bench.err || { tail -20 $D/bench.err; exit 1; }
+      echo "=== rocprofv3 kernel trace $c"
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/prof_kt -o kt -- python3 $R/bench.py $flags --steps 10 > $D/prof_kt.log 2>&1 || { tail -20 $D/prof_kt.log; exit 1; }
+      for pmc in FETCH_SIZE WRITE_SIZE "SQ_INSTS SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES" "SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
+        tag=$(echo $pmc | cut -d' ' -f1)
+        echo "=== rocprofv3 --pmc $pmc ($c)"
+        timeout -s KILL 120 rocprofv3 --pmc $pmc --output-format csv -d $D/pmc_$tag -o pmc -- python3 $R/bench.py $flags --steps 3 --warmup 1 > $D/pmc_$tag.log 2>&1 || { tail -20 $D/pmc_$tag.log; exit 1; }
+      done
     done
     cd $R ;;
   esac

@@ -1,0 +1,108 @@
+#!/usr/bin/env python3
+"""Recompute the bench line's `roofline` fields from a committed profile directory.
+
+  python tools/roofline.py profiles/r2/cfg2 [--write profiles/solve_kernel_counters.json]
+
+The directory holds what tools/gpu_run.sh's `prof` step collects for ONE bench config:
+  bench.json                       the bench line of the profiled build (kernel name, B, iterations, peaks)
+  prof_kt/kt_kernel_stats.csv      rocprofv3 --kernel-trace --stats of `bench.py --steps 10`
+  pmc_*/pmc_counter_collection.csv rocprofv3 --pmc passes of `bench.py --steps 3 --warmup 1` (one pass each)
+
+Fields (per launch of the dominant solve kernel; the first dispatch of every pass is the warmup and skipped):
+  kernel_ms          kernel-trace average duration (the bench's own HIP-event figure must agree)
+  achieved / frac    algorithmic FP64 flops per launch (flops_per_iter x instance-iterations) / kernel_ms, / peak
+  traffic            HBM bytes: 2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md: FETCH_SIZE counts half the
+                     bytes of wide reads on gfx950; both in KiB)
+  valu_issue_frac    SQ_INSTS_VALU x 4 cycles / SIMD-cycles (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs): the share of
+                     the chip's vector-issue slots the kernel used (a wave64 VALU op holds a SIMD >= 4 cycles)
+  active_issue_frac  SQ_ACTIVE_INST_ANY / SQ_WAVE_CYCLES: the share of resident-wave time spent issuing
+  mfma_busy_share    SQ_VALU_MFMA_BUSY_CYCLES / SIMD-cycles
+  insts_per_iter     SQ_INSTS / instance-iterations (VALU / SALU / LDS / MFMA split alongside)
+  lds_conflict_share SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+SIMDS, XCDS = 1024, 8
+
+
+def counters(d, kern, skip=1):
+    acc = defaultdict(list)
+    meta = {}
+    for f in sorted(glob.glob(os.path.join(d, "pmc_*", "pmc_counter_collection.csv"))):
+        rows = [r for r in csv.DictReader(open(f)) if r["Kernel_Name"].startswith(kern)]
+        ids = sorted({int(r["Dispatch_Id"]) for r in rows})[skip:]
+        for r in rows:
+            if int(r["Dispatch_Id"]) in ids:
+                acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
+                meta = meta or {k: r[k] for k in ("Grid_Size", "Workgroup_Size", "LDS_Block_Size", "Scratch_Size",
+                                                   "VGPR_Count", "Accum_VGPR_Count", "SGPR_Count")}
+    return {k: sum(v) / len(v) for k, v in acc.items()}, meta
+
+
+def kernel_ms(d, kern):
+    for f in glob.glob(os.path.join(d, "prof_kt", "*kernel_stats.csv")):
+        for r in csv.DictReader(open(f)):
+            if r["Name"].startswith(kern):
+                return float(r["AverageNs"]) * 1e-6, int(r["Calls"])
+    return None, 0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("--write", default=None, help="merge the counter fields into this JSON (bench.py reads it)")
+    a = ap.parse_args()
+    bench = json.load(open(os.path.join(a.dir, "bench.json")))
+    rl = bench["roofline"]
+    kname = rl["kernel"]
+    kern = "void alip::" + kname.replace(",", ", ") if not kname.startswith("void") else kname
+    c, meta = counters(a.dir, kern)
+    ms, calls = kernel_ms(a.dir, kern)
+    its = rl["iters_per_launch"]
+    out = {"kernel": kname, "B": bench["config"]["batch_per_gpu"], "N": bench["config"]["horizon"],
+           "dtype": bench["dtype"], "kernel_ms_trace": ms, "trace_calls": calls, "kernel_ms_bench": rl["kernel_ms"]}
+    if ms:
+        ach = rl["flops_per_iter"] * its / (ms * 1e-3) / 1e12
+        out.update(achieved=ach, peak=rl["peak"], frac=ach / rl["peak"])
+    if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+        out["hbm_bytes_per_launch"] = 1024.0 * (2.0 * c["FETCH_SIZE"] + c["WRITE_SIZE"])
+        out["fetch_kib"], out["write_kib"] = c["FETCH_SIZE"], c["WRITE_SIZE"]
+    if "GRBM_GUI_ACTIVE" in c:
+        simd_cycles = SIMDS * c["GRBM_GUI_ACTIVE"] / XCDS
+        out["simd_cycles"] = simd_cycles
+        if "SQ_INSTS_VALU" in c:
+            out["valu_issue_frac"] = 4.0 * c["SQ_INSTS_VALU"] / simd_cycles
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in c:
+            out["mfma_busy_share"] = c["SQ_VALU_MFMA_BUSY_CYCLES"] / simd_cycles
+        if ms:
+            out["effective_clock_ghz"] = c["GRBM_GUI_ACTIVE"] / XCDS / (ms * 1e-3) / 1e9
+    if "SQ_ACTIVE_INST_ANY" in c and "SQ_WAVE_CYCLES" in c:
+        out["active_issue_frac"] = c["SQ_ACTIVE_INST_ANY"] / c["SQ_WAVE_CYCLES"]
+    if "SQ_WAIT_INST_ANY" in c and "SQ_WAVE_CYCLES" in c:
+        out["wait_inst_frac"] = c["SQ_WAIT_INST_ANY"] / c["SQ_WAVE_CYCLES"]
+    for k in ("SQ_INSTS", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_MFMA"):
+        if k in c:
+            out[k.lower().replace("sq_", "") + "_per_iter"] = c[k] / its
+    if "SQ_LDS_BANK_CONFLICT" in c and c.get("SQ_LDS_IDX_ACTIVE"):
+        out["lds_conflict_share"] = c["SQ_LDS_BANK_CONFLICT"] / c["SQ_LDS_IDX_ACTIVE"]
+    out["scratch_bytes_per_lane"] = int(meta.get("Scratch_Size", -1)) if meta else None
+    out["counters"] = c
+    print(json.dumps(out, indent=1))
+    # the bench line's own fields, for comparison
+    print("bench roofline:", json.dumps({k: rl[k] for k in ("achieved", "peak", "frac", "traffic", "kernel_ms")}),
+          file=sys.stderr)
+    if a.write:
+        db = json.load(open(a.write)) if os.path.exists(a.write) else {}
+        db[f"{kname}|B={out['B']}"] = {k: v for k, v in out.items() if k != "counters"}
+        with open(a.write, "w") as fh:
+            json.dump(db, fh, indent=1)
+
+
+if __name__ == "__main__":
+    main()
