@@ -1583,7 +1583,7 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
         R a = ap;
         R la = uni(llog(ap));   // log a, tracked exactly through the halvings
         bool accepted = false, ftype = false;
-        R ctr[RPL], ta0[RPL], ta1[RPL], vt[RPL][4];
+        R ctr[RPL], ta0[RPL], ta1[RPL];
         R ft = R(0.0), lgt = R(0.0);
         while (a >= amin) {
             RELANE();
@@ -1593,13 +1593,15 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
             bool bad = false;
 #pragma unroll
             for (int q = 0; q < RPL; ++q) {
+                // the trial point is rebuilt from (rv, rdv, a) where needed (on acceptance, the same fma)
+                R vt[4];
 #pragma unroll
-                for (int i = 0; i < 4; ++i) vt[q][i] = fma(a, rdv[q][i], rv[q][i]);
+                for (int i = 0; i < 4; ++i) vt[i] = fma(a, rdv[q][i], rv[q][i]);
                 R o[6];
 #pragma unroll
                 for (int i = 0; i < 6; ++i) o[i] = w.obs6[6 * roi[q] + i];
-                row_trans(rtype[q], vt[q], w.cst[K_GXG], w.cst[K_GYG], ta0[q], ta1[q]);
-                ctr[q] = row_value(rtype[q], rk[q], vt[q], ta0[q], ta1[q], o, CK);
+                row_trans(rtype[q], vt, w.cst[K_GXG], w.cst[K_GYG], ta0[q], ta1[q]);
+                ctr[q] = row_value(rtype[q], rk[q], vt, ta0[q], ta1[q], o, CK);
                 const R st = sr[q] + a * dS[q];
                 if (rtype[q] < R_NONE) tht += fabs(ctr[q] - st);
                 if (rtype[q] == R_OBJ) ft += ctr[q];
@@ -1654,7 +1656,7 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
 #pragma unroll
             for (int q = 0; q < RPL; ++q) {
 #pragma unroll
-                for (int i = 0; i < 4; ++i) rv[q][i] = vt[q][i];
+                for (int i = 0; i < 4; ++i) rv[q][i] = fma(a, rdv[q][i], rv[q][i]);
                 ra0[q] = ta0[q];
                 ra1[q] = ta1[q];
                 sr[q] += a * dS[q];
