@@ -220,7 +220,12 @@ int alipmpc_rollout_batch(void* handle, int64_t B, int32_t S,
  * (the reference starts at -1), obstacles as alipmpc_solve_batch.  Outputs (any may be NULL):
  *   foot_traj B x S x 3 (p_list[0] of each step's last solve, NaN after the stop), x_traj B x (S+1) x 5
  *   (touchdown states), hd_traj B x S x 2 (hd_input_pr, hd_input_cos of each step), status_traj / iters_traj
- *   B x S x f_cyc (ALIPMPC_ROLLOUT_DONE after the stop), steps_to_goal B (-1: not within S).
+ *   B x S x f_cyc (ALIPMPC_ROLLOUT_DONE after the stop), steps_to_goal B (-1: not within S), action_traj
+ *   B x S x f_cyc x 8: the task-space-controller command of every tick (Logger.gen_nex_foot_input +
+ *   gen_tsc_control, logger_mpc.py:318-384: [foot_input x, y, 0, hd_input_pr / f_cyc (i + 4.5) + hd_input_cos,
+ *   nex_pos_fot_loc x, y, nex_vel_fot_loc x, 0] in the Logger's robot-global frame = the map frame moved to the
+ *   initial pose; vel_des starts at alip_des_vel(0.6, leg_ind) and follows mpc_state_tar as main_sim_mpc.py:54,
+ *   88, 112 do; NaN after the stop).
  * LIP variants only (DD: ALIPMPC_EUNSUPPORTED).  Host / device pointers as alipmpc_solve_batch; S * f_cyc solve
  * launches plus two small kernels per tick on the stream.
  */
@@ -228,7 +233,7 @@ int alipmpc_closed_loop_batch(void* handle, int64_t B, int32_t S, int32_t f_cyc,
                               const double* x0, const double* foot0, const double* goal, const int8_t* leg,
                               const double* cir, const int32_t* nc, const double* elp, const int32_t* ne,
                               double* foot_traj, double* x_traj, double* hd_traj, int32_t* status_traj,
-                              int32_t* iters_traj, int32_t* steps_to_goal, void* hip_stream);
+                              int32_t* iters_traj, int32_t* steps_to_goal, double* action_traj, void* hip_stream);
 
 /* Nominal gait of a batch (replaces MPCCBF.alip_des_vel / cal_foot_with_veldes, MPC_LIP_modi.py:181-194, used by
  * the driver at main_sim_mpc.py:54 and the ALIP-only loggers):

@@ -79,7 +79,7 @@ def load(build_if_missing=True):
     L.alipmpc_rollout_batch.argtypes = [P, ctypes.c_int64, ctypes.c_int32] + [P] * 16
     L.alipmpc_rollout_batch.restype = ctypes.c_int
     L.alipmpc_closed_loop_batch.argtypes = [P, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_double,
-                                            ctypes.c_uint64] + [P] * 15
+                                            ctypes.c_uint64] + [P] * 16
     L.alipmpc_closed_loop_batch.restype = ctypes.c_int
     L.alipmpc_trace_len.argtypes = [ctypes.POINTER(Cfg)]
     L.alipmpc_trace_len.restype = ctypes.c_int32
@@ -273,24 +273,25 @@ class Solver:
         """Closed loop at the reference's control rate (alipmpc_closed_loop_batch): B episodes, up to `steps`
         walking steps, f_cyc solves per step on an ALIP plant with an optional seeded velocity kick.
         Returns dict(foot (B,S,3), x (B,S+1,5), hd (B,S,2), status (B,S,f_cyc), iters (B,S,f_cyc),
-        steps_to_goal (B,))."""
+        steps_to_goal (B,), action (B,S,f_cyc,8): the controller command of every tick)."""
         B, x0, goal, leg, cir, nc, elp, ne = self._inputs(x0, goal, leg, cir, nc, elp, ne)
         foot0 = np.ascontiguousarray(foot0, np.float64).reshape(B, 2)
         S, F = int(steps), int(f_cyc)
         out = dict(foot=np.zeros((B, S, 3)), x=np.zeros((B, S + 1, 5)), hd=np.zeros((B, S, 2)),
                    status=np.zeros((B, S, F), np.int32), iters=np.zeros((B, S, F), np.int32),
-                   steps_to_goal=np.zeros(B, np.int32))
+                   steps_to_goal=np.zeros(B, np.int32), action=np.zeros((B, S, F, 8)))
         rc = self._L.alipmpc_closed_loop_batch(self._h, B, S, F, float(kick), int(seed), _ptr(x0), _ptr(foot0),
                                                _ptr(goal), _ptr(leg), _ptr(cir), _ptr(nc), _ptr(elp), _ptr(ne),
                                                _ptr(out["foot"]), _ptr(out["x"]), _ptr(out["hd"]),
                                                _ptr(out["status"]), _ptr(out["iters"]), _ptr(out["steps_to_goal"]),
-                                               None)
+                                               _ptr(out["action"]), None)
         self._check(rc, "alipmpc_closed_loop_batch")
         return out
 
     def closed_loop_device(self, inp, out, steps, f_cyc=40, kick=0.0, seed=0, stream=None):
         """Asynchronous closed loop on device tensors: inp x0 (B,5), foot0 (B,2), goal, leg (int8), cir, nc
-        [, elp, ne]; out dict with any of foot, x, hd, status, iters, steps_to_goal (shapes of closed_loop)."""
+        [, elp, ne]; out dict with any of foot, x, hd, status, iters, steps_to_goal, action (shapes of
+        closed_loop)."""
         import torch
         st = stream if stream is not None else torch.cuda.current_stream()
         B = inp["x0"].shape[0]
@@ -298,7 +299,8 @@ class Solver:
             self._h, B, int(steps), int(f_cyc), float(kick), int(seed), _ptr(inp["x0"]), _ptr(inp["foot0"]),
             _ptr(inp["goal"]), _ptr(inp["leg"]), _ptr(inp["cir"]), _ptr(inp["nc"]), _ptr(inp.get("elp")),
             _ptr(inp.get("ne")), _ptr(out.get("foot")), _ptr(out.get("x")), _ptr(out.get("hd")),
-            _ptr(out.get("status")), _ptr(out.get("iters")), _ptr(out.get("steps_to_goal")), _stream_arg(st))
+            _ptr(out.get("status")), _ptr(out.get("iters")), _ptr(out.get("steps_to_goal")), _ptr(out.get("action")),
+            _stream_arg(st))
         self._check(rc, "alipmpc_closed_loop_batch")
 
     def nominal_gait(self, x, leg=None, vx_max=0.6, vel_des=None):

@@ -3224,6 +3224,11 @@ struct CLP {
     int32_t* status_traj;   // B x S x f
     int32_t* iters_traj;    // B x S x f
     int32_t* steps_to_goal; // B
+    // task-space-controller command per tick (Logger.gen_nex_foot_input / gen_tsc_control), optional
+    double* action_traj;    // B x S x f x 8
+    double* vdes;           // B x 2 v_des_map (main_sim_mpc.py:54, 88, 112)
+    double* pose0;          // B x 3 the initial pose: origin / heading of the Logger's robot-global frame
+    double vdx, vdy0;       // alip_des_vel(0.6, leg_ind) = [vdx, -0.25 * 0.3 * leg_ind * vdy0]
 };
 
 // Logger.angle_A_minus_B (logger_mpc.py:169-175)
@@ -3318,6 +3323,8 @@ __global__ __launch_bounds__(256) void cl_update_kernel(CLP C)
     if (!(fl & 1)) {
         if (C.status_traj) C.status_traj[ti] = ALIPMPC_ROLLOUT_DONE;
         if (C.iters_traj) C.iters_traj[ti] = 0;
+        if (C.action_traj)
+            for (int c = 0; c < 8; ++c) C.action_traj[ti * 8 + c] = NAN;
         if (C.i == C.f - 1) {
             if (C.foot_traj)
                 for (int c = 0; c < 3; ++c) C.foot_traj[((size_t)b * C.S + C.s) * 3 + c] = NAN;
@@ -3346,9 +3353,46 @@ __global__ __launch_bounds__(256) void cl_update_kernel(CLP C)
         const double dx = xp[5 * k] - gx_, dy = xp[5 * k + 1] - gy_;
         close = close || sqrt(dx * dx + dy * dy) <= rad;
     }
-    // the plant moves dt around the stance foot (+ the velocity kick)
     double* x = C.x + 5 * b;
     const double fx = C.pst[2 * b], fy = C.pst[2 * b + 1];
+    if (C.action_traj) {
+        // gen_nex_foot_input (logger_mpc.py:318-360) + gen_tsc_control (:374-384): robot-global frame = the
+        // map frame moved to the initial pose (pos/vel_map_glo_2_robo_glo, :134-150); the foot frame is the
+        // stance foot rotated by the base heading
+        const double* p0 = C.pose0 + 3 * b;
+        double s0, c0;
+        sincos(p0[2], &s0, &c0);
+        auto rob = [&](double px, double py, double& rx, double& ry) {
+            const double dx = px - p0[0], dy = py - p0[1];
+            rx = c0 * dx + s0 * dy;
+            ry = -s0 * dx + c0 * dy;
+        };
+        double nsx, nsy, csx, csy, npx, npy;
+        rob(C.foot[3 * b], C.foot[3 * b + 1], nsx, nsy);       // nex_stf_rob (p_list[0])
+        rob(fx, fy, csx, csy);                                  // pos_stf_rob_glo_frame
+        rob(C.xs[5 * b], C.xs[5 * b + 1], npx, npy);            // nex_pos_rob (x_nex of this tick)
+        const double vx = C.vdes[2 * b], vy = C.vdes[2 * b + 1];
+        const double nvx = c0 * vx + s0 * vy, nvy = -s0 * vx + c0 * vy;   // nex_vel_rob
+        double sb, cb;
+        sincos(x[4] - p0[2], &sb, &cb);                         // M_T of hd_base_rob_glo_fram
+        double* a = C.action_traj + ti * 8;
+        a[0] = cb * (nsx - csx) + sb * (nsy - csy);
+        a[1] = -sb * (nsx - csx) + cb * (nsy - csy);
+        a[2] = 0.0;
+        a[3] = hv[1] / C.f * (C.i + 4.5) + (hv[2] - p0[2]);    // hd_input_pr ramp + hd_input_cos (robot frame)
+        a[4] = cb * (npx - csx) + sb * (npy - csy);
+        a[5] = -sb * (npx - csx) + cb * (npy - csy);
+        a[6] = cb * nvx + sb * nvy;
+        a[7] = 0.0;
+        (void)nvy;
+    }
+    // vel_des <- mpc_state_tar[0][2:4] after every solve, [1][2:4] at touchdown (main_sim_mpc.py:88, 112)
+    if (C.vdes) {
+        const int kv = (C.i == C.f - 1 && C.N > 1) ? 1 : 0;
+        C.vdes[2 * b] = xp[5 * kv + 2];
+        C.vdes[2 * b + 1] = xp[5 * kv + 3];
+    }
+    // the plant moves dt around the stance foot (+ the velocity kick)
     double xn[5];
     xn[0] = C.ch_d * x[0] + C.shb_d * x[2] + (1.0 - C.ch_d) * fx;
     xn[1] = C.ch_d * x[1] + C.shb_d * x[3] + (1.0 - C.ch_d) * fy;
@@ -3390,15 +3434,15 @@ __global__ __launch_bounds__(256) void cl_init_kernel(CLP C)
     if (C.steps_to_goal) C.steps_to_goal[b] = -1;
     if (C.x_traj)
         for (int c = 0; c < 5; ++c) C.x_traj[(size_t)b * (C.S + 1) * 5 + c] = C.x[5 * b + c];
+    if (C.vdes) {   // vel_des = alip_des_vel(0.6, leg_ind) (main_sim_mpc.py:54)
+        C.vdes[2 * b] = C.vdx;
+        C.vdes[2 * b + 1] = 0.5 * (-0.5 * (double)C.leg[b] * 0.3) * C.vdy0;
+        C.pose0[3 * b] = C.x[5 * b];
+        C.pose0[3 * b + 1] = C.x[5 * b + 1];
+        C.pose0[3 * b + 2] = C.x[5 * b + 4];
+    }
 }
 
-// ------------------------------------------------------------------------------------------------
-// dense CoM traces of a plan (the pos_det output of MPCCBF.gen_control_test, MPC_LIP_modi.py:117-122,
-// 304-322): for step k, rows [x_k[0:2]; pos(t_i)], t_i = i * 0.01 (np.arange(0, dt + 0.01, 0.01)), of the
-// continuous ALIP flow from x_k around the stance foot p_k:  pos(t) = ch x_k[0:2] + sh/beta x_k[2:4] +
-// (1 - ch) p_k[0:2].  x_{k+1} = M_A x_k + M_B u_k and p_k = W (u_k - A x_k) as gen_control_test forms them.
-// One thread per output row (coalesced 16-byte stores); HBM-bound: 40 B of plan in, rows x 16 B out.
-// ------------------------------------------------------------------------------------------------
 // nominal gait (MPC_LIP_modi.py:181-194): vel_des = alip_des_vel(vx_max, leg_ind) unless a target velocity is
 // given, foot = cal_foot_with_veldes(x, vel_des) = B_vel^-1 (vel_des - (A x)[2:4]) with B_vel = -beta sinh(beta T) I
 struct NgP {
@@ -3433,6 +3477,13 @@ __global__ __launch_bounds__(256) void nominal_gait_kernel(NgP Q)
     Q.foot[2 * b + 1] = Q.ibv * (v1 - ay);
 }
 
+// ------------------------------------------------------------------------------------------------
+// dense CoM traces of a plan (the pos_det output of MPCCBF.gen_control_test, MPC_LIP_modi.py:117-122,
+// 304-322): for step k, rows [x_k[0:2]; pos(t_i)], t_i = i * 0.01 (np.arange(0, dt + 0.01, 0.01)), of the
+// continuous ALIP flow from x_k around the stance foot p_k:  pos(t) = ch x_k[0:2] + sh/beta x_k[2:4] +
+// (1 - ch) p_k[0:2].  x_{k+1} = M_A x_k + M_B u_k and p_k = W (u_k - A x_k) as gen_control_test forms them.
+// One thread per output row (coalesced 16-byte stores); HBM-bound: 40 B of plan in, rows x 16 B out.
+// ------------------------------------------------------------------------------------------------
 struct TrP {
     long long B;
     int N, rows;        // rows per step = 1 + samples
@@ -4489,7 +4540,7 @@ int alipmpc_closed_loop_batch(void* handle, int64_t B, int32_t S, int32_t f_cyc,
                               const double* x0, const double* foot0, const double* goal, const int8_t* leg,
                               const double* cir, const int32_t* nc, const double* elp, const int32_t* ne,
                               double* foot_traj, double* x_traj, double* hd_traj, int32_t* status_traj,
-                              int32_t* iters_traj, int32_t* steps_to_goal, void* hip_stream)
+                              int32_t* iters_traj, int32_t* steps_to_goal, double* action_traj, void* hip_stream)
 {
     Handle* h = (Handle*)handle;
     if (!h) return ALIPMPC_EINVAL;
@@ -4510,9 +4561,11 @@ int alipmpc_closed_loop_batch(void* handle, int64_t B, int32_t S, int32_t f_cyc,
             int8_t *leg, *sleg;
             uint8_t *flags, *act;
             int32_t *st, *it;
-            double *goal, *cir, *elp, *ft, *xt, *hd;
+            double *goal, *cir, *elp, *ft, *xt, *hd, *actd;
             int32_t *nc, *ne, *stt, *itt, *sg;
+            double *vdes, *pose0;
         } l{};
+        l.vdes = cv.take<double>(Bz * 2); l.pose0 = cv.take<double>(Bz * 3);
         l.x = cv.take<double>(Bz * 5); l.pst = cv.take<double>(Bz * 2); l.hdv = cv.take<double>(Bz * 4);
         l.mhd = cv.take<double>(Bz * 3); l.plan = cv.take<double>(Bz * n); l.xs = cv.take<double>(Bz * 5);
         l.u0 = cv.take<double>(Bz * n); l.u = cv.take<double>(Bz * n); l.foot = cv.take<double>(Bz * 3);
@@ -4525,6 +4578,7 @@ int alipmpc_closed_loop_batch(void* handle, int64_t B, int32_t S, int32_t f_cyc,
             l.ft = cv.take<double>(Bz * Sz * 3); l.xt = cv.take<double>(Bz * (Sz + 1) * 5);
             l.hd = cv.take<double>(Bz * Sz * 2); l.stt = cv.take<int32_t>(Bz * Sz * Fz);
             l.itt = cv.take<int32_t>(Bz * Sz * Fz); l.sg = cv.take<int32_t>(Bz);
+            if (action_traj) l.actd = cv.take<double>(Bz * Sz * Fz * 8);
         }
         return l;
     };
@@ -4551,6 +4605,7 @@ int alipmpc_closed_loop_batch(void* handle, int64_t B, int32_t S, int32_t f_cyc,
     const int32_t *d_nc = nc, *d_ne = ne;
     double *d_ft = foot_traj, *d_xt = x_traj, *d_hd = hd_traj;
     int32_t *d_stt = status_traj, *d_itt = iters_traj, *d_sg = steps_to_goal;
+    double* d_act = action_traj;
     if (host) {
         HIPCHK(h, hipMemcpyAsync(l.goal, goal, Bz * 2 * 8, hipMemcpyHostToDevice, st));
         if (cf.nc_max) HIPCHK(h, hipMemcpyAsync(l.cir, cir, Bz * 3 * cf.nc_max * 8, hipMemcpyHostToDevice, st));
@@ -4565,6 +4620,7 @@ int alipmpc_closed_loop_batch(void* handle, int64_t B, int32_t S, int32_t f_cyc,
         d_ft = foot_traj ? l.ft : nullptr; d_xt = x_traj ? l.xt : nullptr; d_hd = hd_traj ? l.hd : nullptr;
         d_stt = status_traj ? l.stt : nullptr; d_itt = iters_traj ? l.itt : nullptr;
         d_sg = steps_to_goal ? l.sg : nullptr;
+        d_act = action_traj ? l.actd : nullptr;
     }
     CLP C;
     std::memset(&C, 0, sizeof(C));
@@ -4574,7 +4630,13 @@ int alipmpc_closed_loop_batch(void* handle, int64_t B, int32_t S, int32_t f_cyc,
     C.status = l.st; C.iters = l.it; C.active = l.act;
     C.foot_traj = d_ft; C.x_traj = d_xt; C.hd_traj = d_hd; C.status_traj = d_stt; C.iters_traj = d_itt;
     C.steps_to_goal = d_sg;
+    C.action_traj = d_act; C.vdes = l.vdes; C.pose0 = l.pose0;
     const double beta = std::sqrt(cf.g / cf.H), T = cf.dt, dt = T / f_cyc;
+    {   // alip_des_vel(0.6, leg_ind) (MPC_LIP_modi.py:181-186)
+        const double sh = std::sinh(beta * T), ch = std::cosh(beta * T);
+        C.vdx = beta / std::tanh(T * beta / 2) * 0.6 * T / 2;
+        C.vdy0 = (beta * sh) / (ch + 1);
+    }
     C.ch_d = std::cosh(beta * dt); C.shb_d = std::sinh(beta * dt) / beta; C.bsh_d = std::sinh(beta * dt) * beta;
     C.td = dt / T;
     const unsigned g1 = (unsigned)((B + 255) / 256);
@@ -4610,6 +4672,7 @@ int alipmpc_closed_loop_batch(void* handle, int64_t B, int32_t S, int32_t f_cyc,
         if (foot_traj) HIPCHK(h, hipMemcpyAsync(foot_traj, l.ft, Bz * Sz * 3 * 8, hipMemcpyDeviceToHost, st));
         if (x_traj) HIPCHK(h, hipMemcpyAsync(x_traj, l.xt, Bz * (Sz + 1) * 5 * 8, hipMemcpyDeviceToHost, st));
         if (hd_traj) HIPCHK(h, hipMemcpyAsync(hd_traj, l.hd, Bz * Sz * 2 * 8, hipMemcpyDeviceToHost, st));
+        if (action_traj) HIPCHK(h, hipMemcpyAsync(action_traj, l.actd, Bz * Sz * Fz * 8 * 8, hipMemcpyDeviceToHost, st));
         if (status_traj) HIPCHK(h, hipMemcpyAsync(status_traj, l.stt, Bz * Sz * Fz * 4, hipMemcpyDeviceToHost, st));
         if (iters_traj) HIPCHK(h, hipMemcpyAsync(iters_traj, l.itt, Bz * Sz * Fz * 4, hipMemcpyDeviceToHost, st));
         if (steps_to_goal) HIPCHK(h, hipMemcpyAsync(steps_to_goal, l.sg, Bz * 4, hipMemcpyDeviceToHost, st));

@@ -296,6 +296,20 @@ def closed_loop_batch(cfg, x0, foot0, goal, leg, cir, nc, elp=None, ne=None, ste
     xs = np.zeros((B, S + 1, 5))
     xs[:, 0] = x
     hd = np.zeros((B, S, 2))
+    # controller command per tick (Logger.gen_nex_foot_input / gen_tsc_control, logger_mpc.py:318-384): the
+    # robot-global frame is the map frame moved to the initial pose (pos/vel_map_glo_2_robo_glo, :134-150);
+    # vel_des = alip_des_vel(0.6, leg_ind) first (main_sim_mpc.py:54), then mpc_state_tar[0][2:4] after each
+    # solve and [1][2:4] at touchdown (:88, :112)
+    action = np.full((B, S, F, 8), np.nan)
+    pose0 = np.concatenate([x[:, 0:2], x[:, 4:5]], axis=1).copy()
+    beta_ = math.sqrt(cfg.g / cfg.H)
+    sh_, ch_ = math.sinh(beta_ * cfg.dt), math.cosh(beta_ * cfg.dt)
+    vdx = beta_ / math.tanh(cfg.dt * beta_ / 2) * 0.6 * cfg.dt / 2
+    vdes = np.stack([np.full(B, vdx), 0.5 * (-0.5 * legv.astype(float) * 0.3) * ((beta_ * sh_) / (ch_ + 1))], 1)
+
+    def rot(th, vx, vy):
+        c, s_ = np.cos(th), np.sin(th)
+        return c * vx + s_ * vy, -s_ * vx + c * vy
     status = np.full((B, S, F), -10, np.int32)
     iters = np.zeros((B, S, F), np.int32)
     stg = np.full(B, -1, np.int32)
@@ -349,6 +363,19 @@ def closed_loop_batch(cfg, x0, foot0, goal, leg, cir, nc, elp=None, ne=None, ste
                 close = (d <= 0.35).any(1)
             else:
                 close = d[:, 0] <= (0.15 if cfg.variant == VARIANT_MODI else 0.35)
+            p0 = pose0[idx]
+            nsx, nsy = rot(p0[:, 2], o["foot"][:, 0] - p0[:, 0], o["foot"][:, 1] - p0[:, 1])
+            csx, csy = rot(p0[:, 2], fx - p0[:, 0], fy - p0[:, 1])
+            npx, npy = rot(p0[:, 2], xn[:, 0] - p0[:, 0], xn[:, 1] - p0[:, 1])
+            nvx, nvy = rot(p0[:, 2], vdes[idx, 0], vdes[idx, 1])
+            fi = rot(xi[:, 4] - p0[:, 2], nsx - csx, nsy - csy)
+            npf = rot(xi[:, 4] - p0[:, 2], npx - csx, npy - csy)
+            nvf = rot(xi[:, 4] - p0[:, 2], nvx, nvy)
+            z = np.zeros(len(idx))
+            action[idx, s, i] = np.stack([fi[0], fi[1], z, hp / F * (i + 4.5) + (hdv[idx, 2] - p0[:, 2]), npf[0], npf[1],
+                                          nvf[0], z], axis=1)
+            kv = 1 if (i == F - 1 and N > 1) else 0
+            vdes[idx] = xp[:, kv, 2:4]
             xa = np.stack([ch_d * xi[:, 0] + shb_d * xi[:, 2] + (1.0 - ch_d) * fx,
                            ch_d * xi[:, 1] + shb_d * xi[:, 3] + (1.0 - ch_d) * fy,
                            bsh_d * xi[:, 0] + ch_d * xi[:, 2] - bsh_d * fx,
@@ -368,4 +395,4 @@ def closed_loop_batch(cfg, x0, foot0, goal, leg, cir, nc, elp=None, ne=None, ste
                 stg[stop] = s + 1
             rclose[idx] |= close
         xs[:, s + 1] = x
-    return dict(foot=foot, x=xs, hd=hd, status=status, iters=iters, steps_to_goal=stg)
+    return dict(foot=foot, x=xs, hd=hd, status=status, iters=iters, steps_to_goal=stg, action=action)

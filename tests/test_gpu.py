@@ -853,6 +853,18 @@ def test_closed_loop_matches_oracle(gpu_lib, coracle, variant, kick, program):
     # the first step's heading inputs depend on the initial state alone
     np.testing.assert_allclose(o["hd"][:, 0], ref["hd"][:, 0], rtol=0, atol=1e-12)
     np.testing.assert_allclose(o["x"][:, 0], x0, rtol=0, atol=0)
+    # controller commands (gen_nex_foot_input + gen_tsc_control per tick): NaN exactly after the stops, and
+    # equal to the oracle's on the steps both loops entered from the same touchdown state with the same turn
+    # input, at ticks where this and the previous solve took the same path (status, iteration count)
+    assert np.array_equal(np.isnan(o["action"]).all(-1), o["status"] == gpu_lib.ROLLOUT_DONE)
+    S_, F_ = o["status"].shape[1:]
+    step_ok = (np.abs(o["x"][:, :S_] - ref["x"][:, :S_]).max(-1) <= 1e-9) & (np.abs(o["hd"] - ref["hd"]).max(-1) <= 1e-9)
+    st_same = (o["status"] == ref["status"]) & (o["iters"] == ref["iters"]) & (o["status"] >= 0)
+    prev = np.concatenate([np.ones((B, S_, 1), bool), st_same[:, :, :-1]], axis=2)
+    same = st_same & prev & step_ok[:, :, None]
+    aerr = np.abs(o["action"] - ref["action"]).max(-1)[same]
+    assert same.mean() >= 0.4, same.mean()
+    assert (aerr <= 1e-6).mean() >= 0.95 and np.median(aerr) <= 1e-9, ((aerr <= 1e-6).mean(), np.median(aerr))
     assert (o["steps_to_goal"][:12] > 0).sum() >= 4
     done = o["status"] == gpu_lib.ROLLOUT_DONE
     for b in np.nonzero(o["steps_to_goal"] > 0)[0]:

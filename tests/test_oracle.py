@@ -329,6 +329,21 @@ def test_closed_loop_oracle_semantics(coracle, variant):
     first = coracle.solve_batch(cfg, xn0, bt["goal"], -leg, bt["cir"], bt["nc"], None, None, np.tile(xn0, (1, 3)))
     assert np.array_equal(r["status"][:, 0, 0], first["status"])
     assert np.array_equal(r["iters"][:, 0, 0], first["iters"])
+    # tick 0's controller command = the Logger's formulas (alipmpc.tsc, pinned to g5_logger) on the same inputs:
+    # robot frame at the initial pose, vel_des = alip_des_vel(0.6, leg_ind), base angle 0 in that frame
+    from alipmpc import tsc
+    mp_des = np.stack([np.full(B, 0.0), np.zeros(B)], 1)
+    beta_ = math.sqrt(9.81)
+    sig = beta_ / math.tanh(0.4 * beta_ / 2)
+    mp_des[:, 0] = sig * 0.6 * 0.4 / 2
+    mp_des[:, 1] = 0.5 * (-0.5 * leg.astype(float) * 0.3) * (beta_ * math.sinh(beta_ * 0.4)) / (math.cosh(beta_ * 0.4) + 1)
+    nex_stf = tsc.map_to_robot_pos(first["foot"][:, 0:2], x0[:, 0:2], x0[:, 4])
+    cur_stf = tsc.map_to_robot_pos(foot0, x0[:, 0:2], x0[:, 4])
+    nex_pos = tsc.map_to_robot_pos(xn0[:, 0:2], x0[:, 0:2], x0[:, 4])
+    nex_vel = tsc.map_to_robot_vel(mp_des, x0[:, 4])
+    fi, npf, nvf = tsc.foot_frame_inputs(nex_stf, cur_stf, np.zeros(B), nex_pos, nex_vel)
+    act0 = tsc.gen_tsc_control(fi, npf, nvf, r["hd"][:, 0, 0], r["hd"][:, 0, 1] - x0[:, 4], 0, F)
+    np.testing.assert_allclose(r["action"][:, 0, 0], act0, rtol=0, atol=1e-12)
     for b in range(B):
         stance = foot0[b]
         for s in range(S):
