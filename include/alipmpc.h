@@ -270,8 +270,10 @@ int alipmpc_trace_batch(void* handle, int64_t B, const double* x0, const double*
 int alipmpc_solve_slots(void* handle, int64_t* slots);
 
 /* The device program this handle's solves run (cfg.program): "solve_kernel<N,rows/4,type>" (one instance per
- * wavefront), "lane_kernel<N,circle slots,modi,type>" (one instance per lane) or "dd_solve_kernel<N,row
- * groups>".  No reference counterpart.  The string is owned by the library. */
+ * wavefront; launched as one wave per instance when the batch fits alipmpc_solve_slots, as the persistent
+ * work queue otherwise — the same bits per instance either way), "lane_kernel<N,circle slots,modi,type>" (one
+ * instance per lane) or "dd_solve_kernel<N,row groups>".  No reference counterpart.  The string is owned by
+ * the library. */
 const char* alipmpc_solve_program(void* handle);
 
 /* Duration in milliseconds of the most recent solve kernel launch on this handle, measured with HIP

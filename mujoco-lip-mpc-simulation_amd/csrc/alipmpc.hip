@@ -427,7 +427,7 @@ __device__ __forceinline__ void sabs(double x, double eps, double& v, double& d1
 }
 
 template <int N, bool JAC>
-__device__ double row_eval(const KP& P, const RowInfo& ri, const double* V, const double* CT, const double* ST,
+__device__ __forceinline__ double row_eval(const KP& P, const RowInfo& ri, const double* V, const double* CT, const double* ST,
                            const double* obs, double eps, double* coef, int* gen)
 {
     const int k = ri.k;
@@ -1809,12 +1809,16 @@ __device__ __forceinline__ void queue_exit(uint32_t* q)
 template <int KSM, class R>
 constexpr int solve_waves() { return 4 * KSM > WAVE ? ALIP_WAVES_RPL2 : (sizeof(R) == 4 ? ALIP_WAVES_F32 : ALIP_WAVES_RPL1); }
 
-// One program per configuration: every solve launch is a grid of at most the resident workgroups whose
-// waves take instances from the launch's work queue, whatever the batch size.  An instance's arithmetic
-// therefore does not depend on B or on the device's slot count (a batch solved whole or in chunks gives
-// bit-identical results), and a wave that finishes a short solve takes the next instance at once instead
-// of idling until its workgroup's longest solve ends (a workgroup's slots are only refilled as a whole).
-template <int N, int KSM, class R>
+// Launch forms of one solve program.  A batch larger than the resident slots runs the persistent work queue:
+// a grid of the resident workgroups whose waves take instances with one atomicAdd each, so a wave that
+// finishes a short solve takes the next instance at once instead of idling until its workgroup's longest
+// solve ends.  A batch that fits the slots (B <= alipmpc_solve_slots, cfg2) needs no queue: one instance per
+// wave, no instance loop — the loop-carried values of the persistent form cost registers (scratch 76 -> 44
+// B/lane) and 11 % of the cfg2 launch (tools/ab_solve.py, profiles/r2).  Both forms inline the same
+// solve_one and produce the same bits for an instance (test_work_queue_batch_independence solves a batch
+// above the slots whole and in half-slot chunks and compares status, iters, u, foot, x_pred exactly), so an
+// instance's result does not depend on its batch or on the device's slot count.
+template <int N, int KSM, class R, bool ONE>
 __global__ __launch_bounds__(256, (solve_waves<KSM, R>())) void solve_kernel(KP Pv)
 {
     using D = Dim<N>;
@@ -1831,10 +1835,15 @@ __global__ __launch_bounds__(256, (solve_waves<KSM, R>())) void solve_kernel(KP 
     __syncthreads();
     const KP& P = *Ps;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);   // wave-uniform (SGPR)
-    uint32_t* const q = Pv.queue;
-    for (long long b = next_instance(q); b < Pv.B; b = next_instance(q))
-        if (!Pv.active || Pv.active[b]) solve_one<N, KSM, R, true>(P, G, E, wsb, wv, b);   // rollout: skip finished
-    queue_exit(q);
+    if constexpr (ONE) {
+        const long long b = (long long)blockIdx.x * WAVES_PER_BLOCK + wv;
+        if (b < Pv.B && (!Pv.active || Pv.active[b])) solve_one<N, KSM, R, false>(P, G, E, wsb, wv, b);
+    } else {
+        uint32_t* const q = Pv.queue;
+        for (long long b = next_instance(q); b < Pv.B; b = next_instance(q))
+            if (!Pv.active || Pv.active[b]) solve_one<N, KSM, R, true>(P, G, E, wsb, wv, b);   // rollout: skip finished
+        queue_exit(q);
+    }
 }
 
 #include "lane_solve.inc"
@@ -1907,6 +1916,43 @@ __device__ __forceinline__ double gsum16(double v)
     v += dpp<0x141>(v);
     v += dpp<0x140>(v);
     return v;
+}
+
+// one row family of the eval layout for a group: item i = (step k, slot) with cnt slots per step at row offset
+// loff within the step; CIR / ELP slots at or past nsel (selected obstacles) are inactive rows
+template <int N, int TYPE>
+__device__ __forceinline__ void eval_rows(const KP& P, const GWS<N>& w, long long b, int t, int legv, int nsel, int cnt,
+                                          int loff)
+{
+    const size_t mm = (size_t)P.m_max;
+    const int total = N * cnt;
+    for (int i = t; i < total; i += GLANES) {
+        const int k = cnt == 1 ? i : i / cnt, slot = i - k * cnt;
+        const int r = k * P.rps + loff + slot;
+        const bool act = (TYPE != R_CIR && TYPE != R_ELP) || slot < nsel;
+        RowInfo ri;
+        ri.type = TYPE;
+        ri.k = k;
+        ri.slot = slot;
+        double cf[4];
+        int gn[4];
+        double c = row_eval<N, true>(P, ri, w.V, w.CT, w.ST, w.obs, 0.0, cf, gn);
+        if (!act) {
+            c = 0.0;
+            cf[0] = cf[1] = cf[2] = cf[3] = 0.0;
+            gn[0] = gn[1] = gn[2] = gn[3] = 0;
+            ri.type = R_NONE;
+        }
+        st4(w.rcoef + 4 * r, cf[0], cf[1], cf[2], cf[3]);
+        *reinterpret_cast<uint32_t*>(w.rgen + 4 * r) =
+            (uint32_t)gn[0] | ((uint32_t)gn[1] << 8) | ((uint32_t)gn[2] << 16) | ((uint32_t)gn[3] << 24);
+        double clv, cuv;
+        row_bounds(P, ri, legv, clv, cuv);
+        if (P.c_out) gptr(P.c_out)[b * mm + r] = c;
+        if (P.cl_out) gptr(P.cl_out)[b * mm + r] = clv;
+        if (P.cu_out) gptr(P.cu_out)[b * mm + r] = cuv;
+        if (P.active_out) gptr(P.active_out)[b * mm + r] = act;
+    }
 }
 
 template <int N>
@@ -2046,23 +2092,21 @@ __device__ __forceinline__ void eval_group_one(const KP& P, const GWS<N>& w, con
     }
     const double f = gsum16(fk);
     wave_sync();
-    // rows: values, bounds, activity, generator-form Jacobian rows
+    // rows: values, bounds, activity, generator-form Jacobian rows — one pass per row family (the family is a
+    // compile-time constant in each pass, so no per-row decode and no divergent switch over the families)
     const size_t mm = (size_t)P.m_max;
-    for (int r = t; r < P.mr4; r += GLANES) {
-        const RowInfo ri = decode_row(P, r, ncs, nes);
-        double cf[4];
-        int gn[4];
-        const double c = row_eval<N, true>(P, ri, w.V, w.CT, w.ST, w.obs, 0.0, cf, gn);
-        st4(w.rcoef + 4 * r, cf[0], cf[1], cf[2], cf[3]);
-        *reinterpret_cast<uint32_t*>(w.rgen + 4 * r) =
-            (uint32_t)gn[0] | ((uint32_t)gn[1] << 8) | ((uint32_t)gn[2] << 16) | ((uint32_t)gn[3] << 24);
-        if (r < P.m_max) {
-            double clv, cuv;
-            row_bounds(P, ri, legv, clv, cuv);
-            if (P.c_out) gptr(P.c_out)[b * mm + r] = c;
-            if (P.cl_out) gptr(P.cl_out)[b * mm + r] = clv;
-            if (P.cu_out) gptr(P.cu_out)[b * mm + r] = cuv;
-            if (P.active_out) gptr(P.active_out)[b * mm + r] = ri.type != R_NONE;
+    {
+        const int nc = P.nc_max, ne = P.ne_max, lo = 2 + nc + ne;
+        eval_rows<N, R_VBX>(P, w, b, t, legv, 0, 1, 0);
+        eval_rows<N, R_VBY>(P, w, b, t, legv, 0, 1, 1);
+        if (nc) eval_rows<N, R_CIR>(P, w, b, t, legv, ncs, nc, 2);
+        if (ne) eval_rows<N, R_ELP>(P, w, b, t, legv, nes, ne, 2 + nc);
+        eval_rows<N, R_LEG>(P, w, b, t, legv, 0, 1, lo);
+        eval_rows<N, R_DTH>(P, w, b, t, legv, 0, 1, lo + 1);
+        if (P.rps > lo + 2) eval_rows<N, R_FEN>(P, w, b, t, legv, 0, 1, lo + 2);
+        for (int r = P.m_max + t; r < P.mr4; r += GLANES) {   // padding rows: zero coefficients for the J steps
+            st4(w.rcoef + 4 * r, 0.0, 0.0, 0.0, 0.0);
+            *reinterpret_cast<uint32_t*>(w.rgen + 4 * r) = 0u;
         }
     }
     wave_sync();
@@ -3582,35 +3626,35 @@ void launch_solve(const KP& P0, size_t smem, hipStream_t st, unsigned* res_out)
 {
     const unsigned need = (unsigned)((P0.B + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
     // KSM = 4-row steps of the J layout, the smallest compiled size covering mo4 rows
-    auto go = [&](auto kern) {
-        set_smem((const void*)kern, smem);
-        const unsigned res = resident_blocks((const void*)kern, smem);
+    auto go = [&](auto kq, auto k1) {
+        set_smem((const void*)kq, smem);
+        set_smem((const void*)k1, smem);
+        const unsigned res = resident_blocks((const void*)kq, smem);
         if (res_out) {   // query only (alipmpc_solve_slots)
             *res_out = res;
             return;
         }
-        // a persistent grid of at most the resident workgroups (the work queue hands out the instances)
-        unsigned grid = res > 0 && res < need ? res : need;
-#ifdef ALIP_DEV_GRID
-        static const unsigned cap = (unsigned)atoi(getenv("ALIP_GRID") ? getenv("ALIP_GRID") : "0");
-        if (cap > 0 && grid > cap) grid = cap;
-#endif
-        hipLaunchKernelGGL(kern, dim3(grid), dim3(WAVE * WAVES_PER_BLOCK), smem, st, P0);
+        if (res > 0 && need > res)   // the persistent work queue over the resident workgroups
+            hipLaunchKernelGGL(kq, dim3(res), dim3(WAVE * WAVES_PER_BLOCK), smem, st, P0);
+        else                         // every instance has a resident wave: one instance per wave
+            hipLaunchKernelGGL(k1, dim3(need > 0 ? need : 1u), dim3(WAVE * WAVES_PER_BLOCK), smem, st, P0);
     };
+#define ALIP_GO(K) go(solve_kernel<N, K, R, false>, solve_kernel<N, K, R, true>)
     if (P0.mo4 <= 32)
-        go(solve_kernel<N, 8, R>);
+        ALIP_GO(8);
     else if (P0.mo4 <= 40)
-        go(solve_kernel<N, 10, R>);
+        ALIP_GO(10);
     else if (P0.mo4 <= 48)
-        go(solve_kernel<N, 12, R>);
+        ALIP_GO(12);
     else if (P0.mo4 <= 64)
-        go(solve_kernel<N, 16, R>);
+        ALIP_GO(16);
     else if (P0.mo4 <= 96)
-        go(solve_kernel<N, 24, R>);
+        ALIP_GO(24);
     else if (P0.mo4 <= 128)
-        go(solve_kernel<N, 32, R>);
+        ALIP_GO(32);
     else
-        go(solve_kernel<N, 48, R>);
+        ALIP_GO(48);
+#undef ALIP_GO
 }
 
 // solve kernels run in the handle's precision (cfg.precision); the eval hook is always fp64

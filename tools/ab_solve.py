@@ -25,7 +25,11 @@ if len(sys.argv) > 2 and sys.argv[1] == "--one":
         s.solve_device(inp, out, stream=st)
         ms.append(s.last_kernel_ms())
     ms = np.array(ms[3:])
-    print(f"{sys.argv[2]}: median {np.median(ms):.4f} ms  min {ms.min():.4f}  iters {out['iters'].float().mean().item():.3f}", flush=True)
+    import hashlib
+    hsh = hashlib.md5(out["u"].cpu().numpy().tobytes() + out["status"].cpu().numpy().tobytes() +
+                      out["iters"].cpu().numpy().tobytes()).hexdigest()[:12]
+    print(f"{sys.argv[2]}: median {np.median(ms):.4f} ms  min {ms.min():.4f}  iters {out['iters'].float().mean().item():.3f}"
+          f"  outputs {hsh}", flush=True)
 else:
     for rnd in range(2):
         for lib in sys.argv[1:]:

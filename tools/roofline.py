@@ -62,6 +62,7 @@ def main():
     rl = bench["roofline"]
     kname = rl["kernel"]
     kern = "void alip::" + kname.replace(",", ", ") if not kname.startswith("void") else kname
+    kern = kern[:-1] if kern.endswith(">") else kern   # the family: solve_kernel<..., true/false> (launch form)
     c, meta = counters(a.dir, kern)
     ms, calls = kernel_ms(a.dir, kern)
     its = rl["iters_per_launch"]
