@@ -729,9 +729,8 @@ __device__ __forceinline__ bool gj_lds(R* M, int lane)
     }
 #pragma unroll 1
     for (int p = 0; p < n; ++p) {
+        // every read of the step is issued with the pivot's (one LDS round trip per step)
         const R d = M[p * LD + p];
-        if (!(d > R(0))) return false;   // wave-uniform: every lane read the same pivot
-        const R inv = rcp_nr(d);
         R mip[Q], mpj[Q], mij[Q];
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
@@ -739,6 +738,8 @@ __device__ __forceinline__ bool gj_lds(R* M, int lane)
             mpj[q] = M[p * LD + ej[q]];
             mij[q] = M[ei[q] * LD + ej[q]];
         }
+        if (!(d > R(0))) return false;   // wave-uniform: every lane read the same pivot
+        const R inv = rcp_nr(d);
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
             const R f = mpj[q] * inv;
@@ -1052,6 +1053,23 @@ __device__ void hess_blocks(const WSS<N, R>& w, int lane, int rps, int nobs, int
 //   J layout (lane = (g4, col), rows 4s + g4, KSM steps, fully unrolled): J^T y, grad f, J^T w and the
 //   MFMA KKT products.
 // ------------------------------------------------------------------------------------------------
+// sum of the N objective pseudo-rows (rows mr4 .. mr4 + N - 1) of a row-layout value, in step order (the
+// oracle's order): N readlanes instead of a 64-lane reduction
+template <int N, int RPL, class R>
+__device__ __forceinline__ R obj_sum(const R (&v)[RPL], int mr4)
+{
+    R s = R(0);
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        const int r = mr4 + k, q = r / WAVE, l = r - q * WAVE;
+        R x = v[0];
+#pragma unroll
+        for (int qq = 1; qq < RPL; ++qq) x = q == qq ? v[qq] : x;
+        s += bcast(x, l);
+    }
+    return s;
+}
+
 template <int N, int KSM, class R, bool Q>
 __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int wv, long long b)
 {
@@ -1198,10 +1216,10 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
         idu[q] = HU(q) ? R(1.0) / du : R(0.0);
         lg0 += HL(q) ? (HU(q) ? llog(dl * du) : llog(dl)) : (HU(q) ? llog(du) : R(0.0));
         if (rtype[q] < R_NONE) th0 += fabs(cr[q] - sr[q]);
-        if (rtype[q] == R_OBJ) fo += cr[q];
     }
     wsum2(th0, nbl);
-    wsum2(fo, lg0);
+    lg0 = wsum(lg0);
+    fo = obj_sum<N, RPL>(cr, mr4);
     mal = wsum(mal);
     R f_cur = fo, lsum_cur = lg0;
     if (lane == 0) {
@@ -1217,6 +1235,8 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
     int status = -1, it = 0, n_rest = 0;
     int fail_it = -1, it_end = max_iter;   // Error_In_Step_Computation: iteration, and the loop's end
     R e0 = INFINITY;
+    R theta_c = R(0.0);
+    bool theta_ok = false;
     const R gth = R(1e-5), gph = R(1e-8), sth = R(1.1), sph = R(2.3), eta = R(1e-8), gal = R(0.05);
 
     STAMP_DECL
@@ -1290,14 +1310,23 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
 #pragma unroll
             for (int T = 0; T < NT; ++T)
                 if (g4 == 0 && 16 * T + col < n) ru = fmax(ru, fabs(gl[T]));
-            R rcm = R(0.0), nz = R(0.0), comp0 = R(0.0);
+            // complementarity products w = dl zl, du zu: max |w| and, for every candidate mu of the barrier
+            // update, max |w - mu| are attained at the extreme w (|w - mu| is convex in w and fl(w - mu) is
+            // monotone in w), so one max and one min replace a reduction per barrier-update trial
+            R rcm = R(0.0), nz = R(0.0), whi = -INFINITY, wlo = INFINITY;
 #pragma unroll
             for (int q = 0; q < RPL; ++q) {
                 const R dl = sr[q] - cl[q], du = cu[q] - sr[q];
                 if (rtype[q] < R_NONE) rcm = fmax(rcm, fabs(cr[q] - sr[q]));
                 nz += fabs(zl[q]) + fabs(zu[q]);
-                if (HL(q)) comp0 = fmax(comp0, fabs(dl * zl[q]));
-                if (HU(q)) comp0 = fmax(comp0, fabs(du * zu[q]));
+                if (HL(q)) {
+                    whi = fmax(whi, dl * zl[q]);
+                    wlo = fmin(wlo, dl * zl[q]);
+                }
+                if (HU(q)) {
+                    whi = fmax(whi, du * zu[q]);
+                    wlo = fmin(wlo, du * zu[q]);
+                }
             }
             // (max(ru)/sd == max(ru/sd): division by sd > 0 and its rounding are monotone, so the stationarity
             // and feasibility maxima share one reduction)
@@ -1305,7 +1334,10 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
             const R sd = uni(fmax(R(100.0), nz / (w.cst[K_MACT] + n)) / R(100.0));
             const R sc = uni(fmax(R(100.0), nz / fmax(R(1.0), w.cst[K_NBL])) / R(100.0));
             const R base_err = wmax(fmax(ru / sd, rcm));
-            comp0 = wmax(comp0);
+            whi = wmax(whi);
+            wlo = wmin(wlo);
+            const bool anyw = whi >= wlo;
+            const R comp0 = anyw ? fmax(fabs(whi), fabs(wlo)) : R(0.0);
             e0 = uni(fmax(base_err, comp0 / sc));
             if (e0 <= w.cst[K_TOL]) {
                 status = 0;
@@ -1315,14 +1347,7 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
             const R mu_min = w.cst[K_TOL] / R(10.0);
             const R mu_prev = mu;
             for (int t = 0; t < 8; ++t) {
-                R cm = R(0.0);
-#pragma unroll
-                for (int q = 0; q < RPL; ++q) {
-                    const R dl = sr[q] - cl[q], du = cu[q] - sr[q];
-                    if (HL(q)) cm = fmax(cm, fabs(dl * zl[q] - mu));
-                    if (HU(q)) cm = fmax(cm, fabs(du * zu[q] - mu));
-                }
-                cm = wmax(cm);
+                const R cm = anyw ? fmax(fabs(whi - mu), fabs(wlo - mu)) : R(0.0);
                 if (fmax(base_err, cm / sc) <= R(10.0) * mu && mu > mu_min)
                     mu = uni(fmax(mu_min, fmin(R(0.2) * mu, mu * sqrt(mu))));
                 else
@@ -1536,7 +1561,7 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
         // ---- slack / multiplier steps, fraction to boundary
         RELANE();
         R dS[RPL], dZl[RPL], dZu[RPL];
-        R ap = R(1.0), az = R(1.0), theta = R(0.0), sl = R(0.0), gdv = R(0.0);
+        R ap = R(1.0), az = R(1.0), theta = R(0.0), sl = R(0.0), jdv[RPL];
 #pragma unroll
         for (int q = 0; q < RPL; ++q) {
             const int r = lane + WAVE * q;
@@ -1548,7 +1573,7 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
                 ld4(w.rcoef + 4 * r, ca.x, ca.y, cb.x, cb.y);
                 jd = ca.x * rdv[q][0] + ca.y * rdv[q][1] + cb.x * rdv[q][2] + cb.y * rdv[q][3];
             }
-            if (rtype[q] == R_OBJ) gdv += jd;
+            jdv[q] = jd;
             dS[q] = rtype[q] < R_NONE ? jd + rcv[q] : R(0.0);
             dZl[q] = HL(q) ? mu * idl[q] - zl[q] - zl[q] * idl[q] * dS[q] : R(0.0);
             dZu[q] = HU(q) ? mu * idu[q] - zu[q] + zu[q] * idu[q] * dS[q] : R(0.0);
@@ -1563,7 +1588,10 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
         }
         ap = wmin(ap);
         az = wmin(az);
-        wsum2(theta, gdv);
+        // theta = sum |c - s| at the current point: the accepted trial's value (same operations, same order)
+        // unless the point came from the initial set-up or a restoration reset
+        theta = theta_ok ? theta_c : wsum(theta);
+        const R gdv = obj_sum<N, RPL>(jdv, mr4);
         sl = wsum(sl);
         const R phi = uni(f_cur - mu * lsum_cur);
         const R gphi = uni(gdv - mu * sl);
@@ -1584,7 +1612,7 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
         R la = uni(llog(ap));   // log a, tracked exactly through the halvings
         bool accepted = false, ftype = false;
         R ctr[RPL], ta0[RPL], ta1[RPL];
-        R ft = R(0.0), lgt = R(0.0);
+        R ft = R(0.0), lgt = R(0.0), tht_acc = R(0.0);
         while (a >= amin) {
             RELANE();
             R tht = R(0.0);
@@ -1604,13 +1632,14 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
                 ctr[q] = row_value(rtype[q], rk[q], vt, ta0[q], ta1[q], o, CK);
                 const R st = sr[q] + a * dS[q];
                 if (rtype[q] < R_NONE) tht += fabs(ctr[q] - st);
-                if (rtype[q] == R_OBJ) ft += ctr[q];
+
                 const R d1 = st - cl[q], d2 = cu[q] - st;
                 if (HL(q) && !(d1 > 0)) bad = true;
                 if (HU(q) && !(d2 > 0)) bad = true;
                 lgt += HL(q) ? (HU(q) ? llog(d1 * d2) : llog(d1)) : (HU(q) ? llog(d2) : R(0.0));
             }
-            wsum2(ft, tht);
+            tht = wsum(tht);
+            ft = obj_sum<N, RPL>(ctr, mr4);
             lgt = wsum(lgt);
             const bool anybad = __ballot(bad) != 0ull;
             const R pht = anybad ? INFINITY : ft - mu * lgt;
@@ -1632,6 +1661,7 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
                     ftype = false;
                 }
             }
+            tht_acc = tht;
             if (accepted) break;
             a = uni(a * R(0.5));
             la = uni(la - R(M_LN2));
@@ -1664,7 +1694,10 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
             }
             f_cur = ft;
             lsum_cur = lgt;
+            theta_c = tht_acc;
+            theta_ok = true;
         } else {
+            theta_ok = false;
             // restoration substitute: shortest tried step, slacks reset onto c(u), filter reset
             a = uni(fmax(a, amin));
             vme = fma(a, dvme, vme);
@@ -1690,9 +1723,10 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
                 sr[q] = rtype[q] < R_NONE ? v : R(0.0);
                 const R d1 = sr[q] - cl[q], d2 = cu[q] - sr[q];
                 lr += HL(q) ? (HU(q) ? llog(d1 * d2) : llog(d1)) : (HU(q) ? llog(d2) : R(0.0));
-                if (rtype[q] == R_OBJ) fr += cr[q];
+
             }
-            wsum2(fr, lr);
+            lr = wsum(lr);
+            fr = obj_sum<N, RPL>(cr, mr4);
             f_cur = fr;
             lsum_cur = lr;
             nf = 0;
