@@ -323,8 +323,9 @@ def timed_loop(step, warmup, K, world, dev):
 
 
 def jacobian_sweep(alipmpc, scenes, variant, args, dev, reps=10):
-    """HBM roofline of the unfused Jacobian sweep (eval_kernel: f, grad f, c, J of the
-    reference callbacks at given u) on cfg2-shaped instances (N = 3, 5 circles) whatever --config is.
+    """HBM roofline of the unfused Jacobian sweep (the eval hook: f, grad f, c, J of the reference
+    callbacks at given u; sweep_kernel at N = 3 with circle slots) on cfg2-shaped instances (N = 3, 5 circles)
+    whatever --config is.
     Algorithmic bytes per instance = 8(n + 8 + 3 n_c + 5 n_e) read + 8(1 + n + m + m n) written (n = 5N,
     m = padded rows)."""
     import torch
@@ -355,7 +356,8 @@ def jacobian_sweep(alipmpc, scenes, variant, args, dev, reps=10):
     ms = float(np.mean([a.elapsed_time(b) for a, b in evs[1:]]))
     per = 8 * (n + 8 + 3 * cfg.nc_max) + 8 * (1 + n + m + m * n)
     gbs = Bs * per / (ms * 1e-3) / 1e9
-    return {"kernel": f"eval_kernel<{cfg.N}>", "bound": "hbm", "batch": Bs, "bytes_per_instance": per,
+    kern = f"sweep_kernel<{cfg.nc_max},{'true' if variant == alipmpc.VARIANT_MODI else 'false'}>"   # the eval hook at N=3
+    return {"kernel": kern, "bound": "hbm", "batch": Bs, "bytes_per_instance": per,
             "kernel_ms": ms, "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
             "evals_per_s": Bs / (ms * 1e-3)}
 

@@ -2214,6 +2214,305 @@ __global__ __launch_bounds__(256) void eval_kernel(KP Pv)
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// sweep kernel: the eval hook at N = 3 with circle slots only (cfg2's shape, the bench's Jacobian sweep).
+//   The dense J block (m x 5N doubles) is ~90 % of the bytes an evaluation writes, so the kernel is built
+//   around writing it with full-width stores, with the per-instance set-up shared by 64 instances per
+//   instruction stream:
+//   Phase A (lane = instance, 64 per wave): inputs, select_obs (in-order compaction by rank selects), detour,
+//     the rollout V = E x0 + G u over the structurally non-zero terms of G (x_k depends on u_0..u_{k-1}, p_k on
+//     u_0..u_k; the skipped products are exact zeros), the state pass, f, grad f, and per row the value,
+//     bounds and activity (per-lane stores) and the generator-form coefficients (to LDS).
+//   Phase B (wave-cooperative): element e = lane + 64 s of an instance's J block (row e / 5N, column e % 5N)
+//     is sum_i cf[row][i] * G[gen_i(row)][col]; the G values depend on e only, so one element step runs over
+//     all the blocks with 4 G values in registers, and one store instruction writes 512 contiguous bytes.
+//   The coefficient LDS holds 32 instances: the two halves of the wave's 64 take turns.  The sums are
+//   eval_kernel's, term for term and in the same order (the outputs are bit-identical, tests/test_gpu.py).
+// ------------------------------------------------------------------------------------------------
+template <int NC, bool FEN>
+struct SweepL {
+    static constexpr int N = 3, nu = 15, NG = 32, NCPU = 16;
+    static constexpr int rps = 4 + NC + (FEN ? 1 : 0);
+    static constexpr int m = N * rps;
+    static constexpr int mn = m * nu;
+    static constexpr int S = (mn + WAVE - 1) / WAVE;   // J element steps per instance
+    static constexpr int HALF = WAVE / 2;
+    // one instance slot of the coefficient LDS in dwords: >= 8m and = 52 (mod 64), so the 16 lanes of a
+    // b128 store pass write disjoint bank quads
+    static constexpr int SLOTW = 8 * m + (((52 - 8 * m) % 64) + 64) % 64;
+    static constexpr int SLOTD = SLOTW / 2;
+    static constexpr int GL = NG * NCPU + NG * 5;      // LDS copy of G and E (672 doubles: slots stay aligned)
+    static constexpr size_t smem = sizeof(double) * ((size_t)GL + (size_t)HALF * SLOTD);
+};
+typedef __attribute__((address_space(3))) double ldouble;
+
+// generator rows of row rr of step k in the eval layout [vbx, vby, circles, leg, dtheta, (f_en)] (-1: none)
+template <int NC, bool FEN>
+__device__ __forceinline__ void sweep_gens(int rr, int k, int (&g)[4])
+{
+    g[0] = g[1] = g[2] = g[3] = -1;
+    if (rr < 2 || (FEN && rr == 4 + NC)) {
+        g[0] = gx(k + 1, 2); g[1] = gx(k + 1, 3); g[2] = gx(k + 1, 4);
+        if (rr >= 2) g[3] = gp(k, 2);
+    } else if (rr < 2 + NC) {
+        g[0] = gx(k + 1, 0); g[1] = gx(k + 1, 1); g[2] = gx(k, 0); g[3] = gx(k, 1);
+    } else if (rr == 2 + NC) {
+        g[0] = gx(k, 0); g[1] = gx(k, 1); g[2] = gp(k, 0); g[3] = gp(k, 1);
+    } else {
+        g[0] = gp(k, 2);
+    }
+}
+
+template <int NC, bool FEN>
+__global__ __launch_bounds__(WAVE, 2) void sweep_kernel(KP Pv)
+{
+    using L = SweepL<NC, FEN>;
+    constexpr int N = L::N, nu = L::nu, NG = L::NG, NCPU = L::NCPU, m = L::m, rps = L::rps, S = L::S;
+    constexpr int mn = L::mn, HALF = L::HALF, SLOTD = L::SLOTD;
+    constexpr int NO = NC > 0 ? 3 * NC : 1;
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    double* Gl = smem;
+    double* cfs = smem + L::GL;
+    const int lane = threadIdx.x;
+    for (int i = lane; i < NG * NCPU; i += WAVE) Gl[i] = Pv.G[i];
+    for (int i = lane; i < NG * 5; i += WAVE) Gl[NG * NCPU + i] = Pv.E[i];
+    __syncthreads();
+    const double* const El = Gl + NG * NCPU;
+    gdouble* const Jo = Pv.J_out ? gptr(Pv.J_out) : nullptr;
+    for (long long b0 = (long long)blockIdx.x * WAVE; b0 < Pv.B; b0 += (long long)gridDim.x * WAVE) {
+        // the parameters are read from the kernarg segment where they are used (a laundered constant-space
+        // pointer per chunk): ~100 kernarg SGPRs otherwise stay live across the chunk and spill
+        const __attribute__((address_space(4))) char* kq =
+            (const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(kq));
+        const KP& P = *(const KP*)(const __attribute__((address_space(4))) KP*)kq;
+        // ---------------- phase A: this lane's instance
+        const long long b = b0 + lane;
+        const bool live = b < P.B;
+        const long long bl = live ? b : P.B - 1;
+        double x0v[5], u[nu];
+        const gdouble* x0p = gptr(P.x0) + 5 * bl;
+#pragma unroll
+        for (int c = 0; c < 5; ++c) x0v[c] = x0p[c];
+        const gdouble* up = gptr(P.u0) + (size_t)nu * bl;
+#pragma unroll
+        for (int j = 0; j < nu; ++j) u[j] = up[j];
+        const double g0 = gptr(P.goal)[2 * bl], g1 = gptr(P.goal)[2 * bl + 1];
+        const int legv = P.leg[bl];
+        const int ncr = P.nc[bl];
+        // select_obs (MPC_LIP_modi.py:325-338): the kept circles in input order, compacted by rank
+        double obs[NO];
+#pragma unroll
+        for (int i = 0; i < NO; ++i) obs[i] = 0.0;
+        int nsel = 0;
+#pragma unroll
+        for (int jc = 0; jc < NC; ++jc) {
+            const bool valid = jc < ncr;
+            double c0 = 0, c1 = 0, c2 = 0;
+            if (valid) {
+                const gdouble* c = gptr(P.cir) + ((size_t)bl * NC + jc) * 3;
+                c0 = c[0]; c1 = c[1]; c2 = c[2];
+            }
+            const double d = (x0v[0] - c0) * (x0v[0] - c0) + (x0v[1] - c1) * (x0v[1] - c1) - c2 * c2;
+            const bool keep = valid && (!P.select_obs || d <= P.detect_r2);
+#pragma unroll
+            for (int sl = 0; sl <= jc; ++sl) {
+                const bool here = keep && nsel == sl;
+                obs[3 * sl + 0] = here ? c0 : obs[3 * sl + 0];
+                obs[3 * sl + 1] = here ? c1 : obs[3 * sl + 1];
+                obs[3 * sl + 2] = here ? c2 : obs[3 * sl + 2];
+            }
+            nsel += keep ? 1 : 0;
+        }
+        // detour goal (MPC_LIP_modi.py:247-271): the first selected circle that triggers.  Branch-free: the heading
+        // to the goal and every circle's bearing are independent (one instruction stream, interleaved), then the
+        // first firing circle's side picks the new heading (same functions, same values as eval_kernel)
+        double gxg = g0, gyg = g1;
+        if (P.detour) {
+            const double gd = (x0v[0] - g0) * (x0v[0] - g0) + (x0v[1] - g1) * (x0v[1] - g1);
+            const double th = atan2(g1 - x0v[1], g0 - x0v[0]);
+            bool found = false;
+            double na = 0.0;
+#pragma unroll
+            for (int sl = 0; sl < NC; ++sl) {
+                const double* c = obs + 3 * sl;
+                const double cen = (x0v[0] - c[0]) * (x0v[0] - c[0]) + (x0v[1] - c[1]) * (x0v[1] - c[1]);
+                const double al = atan2(c[1] - x0v[1], c[0] - x0v[0]);
+                double dd = th - al;
+                if (dd < 0 && fabs(dd) > M_PI)
+                    dd += 2 * M_PI;
+                else if (dd > 0 && fabs(dd) > M_PI)
+                    dd -= 2 * M_PI;
+                const bool fire = sl < nsel && cen < gd && cen < 9 * c[2] * c[2] && fabs(dd) < M_PI / 12;
+                na = (fire && !found) ? (dd < 0 ? th - M_PI / 12 : th + M_PI / 12) : na;
+                found = found || fire;
+            }
+            if (found) {
+                const double rr = sqrt(gd);
+                double sn, cs;
+                sincos(na, &sn, &cs);
+                gxg = x0v[0] + rr * cs;
+                gyg = x0v[1] + rr * sn;
+            }
+        }
+        // V = E x0 + G u over the structural non-zeros of G (x_k: u_0..u_{k-1}; p_k: u_0..u_k)
+        double V[NG];
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            const int k = g / 8, c = g % 8;
+            const int lim = c < 5 ? 5 * k : (k < N ? 5 * (k + 1) : 0);
+            if (c >= 5 && k == N) {   // p_N: not a generator of any row
+                V[g] = 0.0;
+                continue;
+            }
+            // one generator row at a time: its (broadcast) LDS reads, then its FMAs — the laundered offset keeps the
+            // reads from being hoisted into one block of hundreds of live VGPRs
+            int og = g * NCPU, oe = g * 5;
+            asm volatile("" : "+v"(og), "+v"(oe));
+            const ldouble* gr = (const ldouble*)Gl + og;
+            const ldouble* er = (const ldouble*)El + oe;
+            double v = 0.0;
+#pragma unroll
+            for (int cc = 0; cc < 5; ++cc) v += er[cc] * x0v[cc];
+#pragma unroll
+            for (int j = 0; j < lim; ++j) v += gr[j] * u[j];
+            asm volatile("" : "+v"(v));   // computed here (not sunk to its uses, which would keep the reads live)
+            V[g] = v;
+        }
+        // state pass: cos/sin theta_k, the objective terms f_k and d f / d V
+        double CT[N + 1], ST[N + 1], fk[N + 1], gfg[N + 1][3];
+        CT[0] = ST[0] = fk[0] = 0.0;
+#pragma unroll
+        for (int k = 1; k <= N; ++k) {
+            const double th = V[gx(k, 4)];
+            double s_, c_;
+            lsincos(th, &s_, &c_);
+            CT[k] = c_;
+            ST[k] = s_;
+            const double px = V[gx(k, 0)], py = V[gx(k, 1)];
+            const double wk = P.q + (k == 1 ? P.p : 0.0);
+            const double ex = px - gxg, ey = py - gyg;
+            const double dxg = gxg - px, dyg = gyg - py;
+            const double phi = th - latan2(dyg, dxg);
+            fk[k] = wk * (ex * ex + ey * ey) + P.r * phi * phi;
+            const double rho2 = dxg * dxg + dyg * dyg;
+            gfg[k][0] = 2 * wk * ex + 2 * P.r * phi * (-dyg / rho2);
+            gfg[k][1] = 2 * wk * ey + 2 * P.r * phi * (dxg / rho2);
+            gfg[k][2] = 2 * P.r * phi;
+        }
+        if (live) {
+            // eval_kernel's 16-lane butterfly sum of f_1..f_3 is f_1 + (f_2 + f_3)
+            if (P.f_out) gptr(P.f_out)[b] = fk[1] + (fk[2] + fk[3]);
+            if (P.goal_eff_out) {
+                gptr(P.goal_eff_out)[2 * b] = gxg;
+                gptr(P.goal_eff_out)[2 * b + 1] = gyg;
+            }
+            // grad f = G^T (d f / d V): the non-zero terms of eval_kernel's sum over g = 8..NG-1, in its order
+            if (P.grad_out) {
+#pragma unroll 1
+                for (int j = 0; j < nu; ++j) {   // a loop: 9 broadcast reads per column, not 135 at once
+                    const ldouble* gc = (const ldouble*)Gl + j;
+                    double gf = 0.0;
+#pragma unroll
+                    for (int k = 1; k <= N; ++k) {
+                        gf += gc[gx(k, 0) * NCPU] * gfg[k][0];
+                        gf += gc[gx(k, 1) * NCPU] * gfg[k][1];
+                        gf += gc[gx(k, 4) * NCPU] * gfg[k][2];
+                    }
+                    gptr(P.grad_out)[(size_t)b * nu + j] = gf;
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+        }
+        // rows: the lanes of one half at a time write their coefficients, then the wave writes those 32 J blocks
+#pragma unroll 1
+        for (int h = 0; h < 2; ++h) {
+            // the row arithmetic of each half stays in its pass (hoisted out of this loop it is live across
+            // phase B and spills)
+#pragma unroll
+            for (int g = 0; g < NG; ++g) asm volatile("" : "+v"(V[g]));
+#pragma unroll
+            for (int k = 0; k <= N; ++k) asm volatile("" : "+v"(CT[k]), "+v"(ST[k]));
+#pragma unroll
+            for (int i = 0; i < NO; ++i) asm volatile("" : "+v"(obs[i]));
+            if ((lane >> 5) == h) {
+                double* slot = cfs + (size_t)(lane & (HALF - 1)) * SLOTD;
+#pragma unroll
+                for (int k = 0; k < N; ++k) {
+#pragma unroll
+                    for (int rr = 0; rr < rps; ++rr) {
+                        const int r = k * rps + rr;
+                        RowInfo ri;
+                        ri.k = k;
+                        ri.slot = rr >= 2 && rr < 2 + NC ? rr - 2 : 0;
+                        ri.type = rr == 0 ? R_VBX
+                                : rr == 1 ? R_VBY
+                                : rr < 2 + NC ? R_CIR
+                                : rr == 2 + NC ? R_LEG
+                                : rr == 3 + NC ? R_DTH : R_FEN;
+                        const bool act = ri.type != R_CIR || ri.slot < nsel;
+                        double cf[4];
+                        int gn[4];
+                        double c = row_eval<N, true>(P, ri, V, CT, ST, obs, 0.0, cf, gn);
+                        if (!act) {
+                            c = 0.0;
+                            cf[0] = cf[1] = cf[2] = cf[3] = 0.0;
+                            ri.type = R_NONE;
+                        }
+                        if (live) {
+                            const size_t o = (size_t)b * m + r;
+                            if (P.c_out) gptr(P.c_out)[o] = c;
+                            if (P.cl_out || P.cu_out) {
+                                double clv, cuv;
+                                row_bounds(P, ri, legv, clv, cuv);
+                                if (P.cl_out) gptr(P.cl_out)[o] = clv;
+                                if (P.cu_out) gptr(P.cu_out)[o] = cuv;
+                            }
+                            if (P.active_out) gptr(P.active_out)[o] = act;
+                        }
+                        if (Jo) st4(slot + 4 * r, cf[0], cf[1], cf[2], cf[3]);
+                    }
+                }
+            }
+            if (!Jo) continue;
+            wave_sync();
+            // ---------------- phase B: the J blocks of this half's instances, one element step s at a time (lane
+            // element e = lane + 64 s: row r = e / 5N, column j = e % 5N, the same in every block), 8 blocks per pass
+            const long long bh = b0 + h * HALF;
+            const int cnt = P.B - bh < HALF ? (int)(P.B - bh) : HALF;
+#pragma unroll 1
+            for (int s = 0; s < S; ++s) {
+                const int e = lane + WAVE * s;
+                if (e < mn) {
+                    const int r = e / nu, j = e - r * nu;
+                    int g[4];
+                    sweep_gens<NC, FEN>(r % rps, r / rps, g);
+                    double gv[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) gv[q] = g[q] >= 0 ? Gl[g[q] * NCPU + j] : 0.0;
+                    const double* cfr = cfs + 4 * r;
+                    gdouble* Jp = Jo + (size_t)bh * mn + e;
+                    int i = 0;
+                    for (; i + 8 <= cnt; i += 8) {
+                        double a[8][4];
+#pragma unroll
+                        for (int q = 0; q < 8; ++q) ld4(cfr + (size_t)(i + q) * SLOTD, a[q][0], a[q][1], a[q][2], a[q][3]);
+#pragma unroll
+                        for (int q = 0; q < 8; ++q)
+                            Jp[(size_t)(i + q) * mn] = a[q][0] * gv[0] + a[q][1] * gv[1] + a[q][2] * gv[2] + a[q][3] * gv[3];
+                    }
+                    for (; i < cnt; ++i) {
+                        double a0, a1, a2, a3;
+                        ld4(cfr + (size_t)i * SLOTD, a0, a1, a2, a3);
+                        Jp[(size_t)i * mn] = a0 * gv[0] + a1 * gv[1] + a2 * gv[2] + a3 * gv[3];
+                    }
+                }
+            }
+            wave_sync();
+        }
+    }
+}
+
 
 // ================================================================================================
 // DD variant: unicycle MPC-CBF (MPC_DD_sig_step.py:123-193 set-up, 320-572 LIP_Prob)
@@ -3810,6 +4109,37 @@ hipError_t launch_lane_f32(int nct, bool modi, const KP& P, hipStream_t st, unsi
 }
 #endif
 
+// sweep kernel (eval hook, N = 3, circles only): one-wave workgroups, a grid-stride over 64-instance chunks on at
+// most the resident workgroups
+hipError_t launch_sweep(int nc, bool fen, const KP& P, hipStream_t st);
+#if ALIP_PART_N(3)
+template <int NC, bool FEN>
+void launch_sweep_t(const KP& P, hipStream_t st)
+{
+    auto kern = sweep_kernel<NC, FEN>;
+    const size_t smem = SweepL<NC, FEN>::smem;
+    set_smem((const void*)kern, smem);
+    const unsigned res = resident_blocks((const void*)kern, smem, WAVE);
+    const unsigned need = (unsigned)((P.B + WAVE - 1) / WAVE);
+    const unsigned grid = res > 0 && res < need ? res : (need > 0 ? need : 1u);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(WAVE), smem, st, P);
+}
+hipError_t launch_sweep(int nc, bool fen, const KP& P, hipStream_t st)
+{
+#define SWCASE(K)                                              \
+    case K:                                                    \
+        fen ? launch_sweep_t<K, true>(P, st) : launch_sweep_t<K, false>(P, st); \
+        break;
+    switch (nc) {
+        SWCASE(0) SWCASE(1) SWCASE(2) SWCASE(3) SWCASE(4) SWCASE(5) SWCASE(6)
+    default:
+        return hipErrorInvalidValue;
+    }
+#undef SWCASE
+    return hipGetLastError();
+}
+#endif
+
 }  // namespace alip
 
 #if ALIP_PART_HOST
@@ -3834,6 +4164,8 @@ struct Handle {
     double* dlk = nullptr;
     float* dlkf = nullptr;
     int lane_nct = -1;
+    // eval hook: the circle-slot count sweep_kernel runs with (-1: eval_kernel serves this configuration)
+    int sweep_nc = -1;
     // work-queue counter pairs of persistent solve launches (a ring: launches in flight on different
     // streams use different pairs; each pair is reset by the last wave of the launch that used it)
     static constexpr unsigned NQ = 64;
@@ -4117,6 +4449,10 @@ hipError_t launch(const Handle* h, bool solve, const KP& P, hipStream_t st, unsi
         }
         return hipErrorInvalidValue;
     }
+    if (!solve && h->sweep_nc >= 0) {
+        if (res_out) return hipErrorInvalidValue;
+        return launch_sweep(h->sweep_nc, h->cfg.variant == ALIPMPC_VARIANT_MODI, P, st);
+    }
     if (solve && h->lane_nct >= 0)
         return f32 ? launch_lane_f32(h->lane_nct, h->cfg.variant == ALIPMPC_VARIANT_MODI, P, st, res_out)
                    : launch_lane_f64(h->lane_nct, h->cfg.variant == ALIPMPC_VARIANT_MODI, P, st, res_out);
@@ -4321,6 +4657,12 @@ int alipmpc_create(const alipmpc_cfg* cfg, int device, void** handle)
             alipmpc_destroy(h);
             return ALIPMPC_EHIP;
         }
+        // the eval hook's sweep kernel: N = 3, circle slots only (ALIPMPC_EVAL_KERNEL=group selects eval_kernel,
+        // for A/B and the bit-identity test)
+        const char* ek = std::getenv("ALIPMPC_EVAL_KERNEL");
+        if (h->cfg.variant != ALIPMPC_VARIANT_DD && h->cfg.N == 3 && h->cfg.ne_max == 0 && h->cfg.nc_max <= 6 &&
+            !(ek && std::strcmp(ek, "group") == 0))
+            h->sweep_nc = h->cfg.nc_max;
         if (h->cfg.program == ALIPMPC_PROGRAM_LANE) {
             h->lane_nct = lane_slots_for(h->cfg);
             if (h->lane_nct < 0) {

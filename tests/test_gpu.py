@@ -933,3 +933,44 @@ def test_nominal_gait_matches_reference_helpers(gpu_lib):
     assert rc == 0
     torch.cuda.synchronize()
     assert np.array_equal(ft.cpu().numpy(), foot) and np.array_equal(vt.cpu().numpy(), vd)
+
+
+@pytest.mark.parametrize("variant,nc,B", [(0, 5, 5003), (1, 5, 4099), (0, 0, 1000), (0, 3, 777), (1, 6, 2048), (0, 6, 65)])
+def test_sweep_kernel_bit_identical_to_group_eval(gpu_lib, variant, nc, B, monkeypatch):
+    """The eval hook's sweep kernel (N = 3, circle slots: lane-per-instance set-up + wave-cooperative J stores)
+    against eval_kernel (16 lanes per instance; ALIPMPC_EVAL_KERNEL=group) on a ragged batch with select_obs /
+    detour on: the same bits for f, grad f, goal, bounds and activity, rounding-level agreement for c and J
+    (fma contraction); both are pinned to the reference callbacks by the tests above.
+    Also: a partial output set through device pointers (the bench's f / grad / c / J) writes the same J."""
+    import torch
+    from alipmpc import scenes
+    bt = scenes.make_batch_vec(B, seed=23 + nc, n_cir=max(nc, 1), N=3)
+    cir = np.ascontiguousarray(bt["cir"][:, :nc]) if nc else np.zeros((B, 0, 3))
+    rng = np.random.default_rng(5)
+    ncnt = np.where(rng.random(B) < 0.3, rng.integers(0, nc + 1, B), np.clip(bt["nc"], 0, nc)).astype(np.int32)
+    u = bt["u0"] + 0.05 * rng.standard_normal(bt["u0"].shape)
+    cfg = gpu_lib.default_cfg(variant, 3, nc_max=nc, ne_max=0)
+    outs = []
+    for kern in ("sweep", "group"):
+        if kern == "group":
+            monkeypatch.setenv("ALIPMPC_EVAL_KERNEL", "group")
+        s = gpu_lib.Solver(cfg)
+        outs.append(s.eval(bt["x0"], bt["goal"], bt["leg"], cir, ncnt, None, None, u))
+    a, g = outs
+    for k in ("f", "grad", "goal_eff", "row_active", "cl", "cu"):
+        assert np.array_equal(a[k], g[k]), k
+    # row values and J rows: the same formulas, but the compiler's fma contraction of a row's arithmetic may differ
+    # between the two kernels (rounding level)
+    for k in ("c", "J"):
+        assert np.max(np.abs(a[k] - g[k]) / np.maximum(1.0, np.abs(g[k]))) <= 1e-14, k
+        assert np.array_equal(a[k] == 0, g[k] == 0), k
+    monkeypatch.delenv("ALIPMPC_EVAL_KERNEL")
+    s = gpu_lib.Solver(cfg)
+    dev = torch.device("cuda", 0)
+    inp = {"x0": torch.from_numpy(bt["x0"]).to(dev), "goal": torch.from_numpy(bt["goal"]).to(dev),
+           "leg": torch.from_numpy(bt["leg"].astype(np.int8)).to(dev), "cir": torch.from_numpy(cir).to(dev),
+           "nc": torch.from_numpy(ncnt).to(dev), "u": torch.from_numpy(u).to(dev)}
+    J = torch.full((B, s.m_max, 15), np.nan, dtype=torch.float64, device=dev)
+    s.eval_device(inp, {"J": J})
+    torch.cuda.synchronize()
+    assert np.array_equal(J.cpu().numpy(), a["J"])

@@ -5,8 +5,10 @@ sys.path.insert(0, os.path.join(ROOT, "mujoco-lip-mpc-simulation_amd"))
 import alipmpc
 from alipmpc import scenes
 dev = torch.device("cuda", 0)
-Bs = 65536
+Bs = int(sys.argv[2]) if len(sys.argv) > 2 else 65536
 cfg = alipmpc.default_cfg(0, 3, nc_max=5, ne_max=0)
+if len(sys.argv) > 1:
+    os.environ["ALIPMPC_EVAL_KERNEL"] = sys.argv[1]   # "group": eval_kernel instead of the sweep kernel
 s = alipmpc.Solver(cfg)
 bt = scenes.make_batch_vec(Bs, seed=7, n_cir=5, N=3, fields=4096)
 n, m = 15, 3 * s.rps
@@ -27,6 +29,7 @@ def t(out, reps=8):
 print("full      ", t(full))
 print("no J      ", t({k: v for k, v in full.items() if k != "J"}))
 print("f only    ", t({"f": full["f"]}))
+print('B', Bs, 'GB/s full', Bs * 4272 / (t(full) * 1e-3) / 1e9)
 x = torch.empty(Bs * 4272 // 8, dtype=torch.float64, device=dev)
 y = torch.empty_like(x)
 for name, fn in (("fill", lambda: x.fill_(1.0)), ("copy", lambda: y.copy_(x))):
