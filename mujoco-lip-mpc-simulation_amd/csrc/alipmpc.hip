@@ -2226,9 +2226,15 @@ __global__ __launch_bounds__(256) void eval_kernel(KP Pv)
 //   Phase B (wave-cooperative): element e = lane + 64 s of an instance's J block (row e / 5N, column e % 5N)
 //     is sum_i cf[row][i] * G[gen_i(row)][col]; the G values depend on e only, so one element step runs over
 //     all the blocks with 4 G values in registers, and one store instruction writes 512 contiguous bytes.
-//   The coefficient LDS holds 32 instances: the two halves of the wave's 64 take turns.  The sums are
-//   eval_kernel's, term for term and in the same order (the outputs are bit-identical, tests/test_gpu.py).
+//   A chunk is CH = 32 instances per wave (lanes 32..63 repeat lanes 0..31 and store nothing), two waves per
+//   workgroup sharing one G/E copy: 2048 waves at B = 65,536, two per SIMD, so one wave's set-up runs under the
+//   other's J stores (the LDS of a 64-instance chunk had allowed one wave per SIMD).  The coefficient LDS holds
+//   CH / 2 instances: the two halves of a chunk take turns.  The sums are eval_kernel's, term for term and in
+//   the same order (the outputs are bit-identical, tests/test_gpu.py).
 // ------------------------------------------------------------------------------------------------
+#ifndef SWEEP_SHAPE_DEFAULT
+#define SWEEP_SHAPE_DEFAULT 322
+#endif
 template <int NC, bool FEN>
 struct SweepL {
     static constexpr int N = 3, nu = 15, NG = 32, NCPU = 16;
@@ -2236,13 +2242,11 @@ struct SweepL {
     static constexpr int m = N * rps;
     static constexpr int mn = m * nu;
     static constexpr int S = (mn + WAVE - 1) / WAVE;   // J element steps per instance
-    static constexpr int HALF = WAVE / 2;
     // one instance slot of the coefficient LDS in dwords: >= 8m and = 52 (mod 64), so the 16 lanes of a
     // b128 store pass write disjoint bank quads
     static constexpr int SLOTW = 8 * m + (((52 - 8 * m) % 64) + 64) % 64;
     static constexpr int SLOTD = SLOTW / 2;
     static constexpr int GL = NG * NCPU + NG * 5;      // LDS copy of G and E (672 doubles: slots stay aligned)
-    static constexpr size_t smem = sizeof(double) * ((size_t)GL + (size_t)HALF * SLOTD);
 };
 typedef __attribute__((address_space(3))) double ldouble;
 
@@ -2263,23 +2267,25 @@ __device__ __forceinline__ void sweep_gens(int rr, int k, int (&g)[4])
     }
 }
 
-template <int NC, bool FEN>
-__global__ __launch_bounds__(WAVE, 2) void sweep_kernel(KP Pv)
+template <int NC, bool FEN, int CH, int WPG>
+__global__ __launch_bounds__(WAVE * WPG, 2) void sweep_kernel(KP Pv)
 {
     using L = SweepL<NC, FEN>;
     constexpr int N = L::N, nu = L::nu, NG = L::NG, NCPU = L::NCPU, m = L::m, rps = L::rps, S = L::S;
-    constexpr int mn = L::mn, HALF = L::HALF, SLOTD = L::SLOTD;
+    constexpr int mn = L::mn, SLOTD = L::SLOTD;
+    constexpr int QI = CH / 2;   // instances per coefficient pass (two passes per chunk)
     constexpr int NO = NC > 0 ? 3 * NC : 1;
+    static_assert(CH == 64 || CH == 32, "instances per wave");
     extern __shared__ __attribute__((aligned(16))) double smem[];
     double* Gl = smem;
-    double* cfs = smem + L::GL;
-    const int lane = threadIdx.x;
-    for (int i = lane; i < NG * NCPU; i += WAVE) Gl[i] = Pv.G[i];
-    for (int i = lane; i < NG * 5; i += WAVE) Gl[NG * NCPU + i] = Pv.E[i];
+    const int wv = threadIdx.x / WAVE, lane = threadIdx.x % WAVE;
+    double* cfs = smem + L::GL + (size_t)wv * QI * SLOTD;
+    for (int i = threadIdx.x; i < NG * NCPU; i += WAVE * WPG) Gl[i] = Pv.G[i];
+    for (int i = threadIdx.x; i < NG * 5; i += WAVE * WPG) Gl[NG * NCPU + i] = Pv.E[i];
     __syncthreads();
     const double* const El = Gl + NG * NCPU;
     gdouble* const Jo = Pv.J_out ? gptr(Pv.J_out) : nullptr;
-    for (long long b0 = (long long)blockIdx.x * WAVE; b0 < Pv.B; b0 += (long long)gridDim.x * WAVE) {
+    for (long long b0 = ((long long)blockIdx.x * WPG + wv) * CH; b0 < Pv.B; b0 += (long long)gridDim.x * WPG * CH) {
         // the parameters are read from the kernarg segment where they are used (a laundered constant-space
         // pointer per chunk): ~100 kernarg SGPRs otherwise stay live across the chunk and spill
         const __attribute__((address_space(4))) char* kq =
@@ -2287,9 +2293,12 @@ __global__ __launch_bounds__(WAVE, 2) void sweep_kernel(KP Pv)
         asm volatile("" : "+s"(kq));
         const KP& P = *(const KP*)(const __attribute__((address_space(4))) KP*)kq;
         // ---------------- phase A: this lane's instance
-        const long long b = b0 + lane;
-        const bool live = b < P.B;
-        const long long bl = live ? b : P.B - 1;
+        // lane % CH owns an instance; lanes >= CH repeat it (same values, no stores): the wave keeps 64 lanes
+        // while a chunk is CH instances, so a batch makes B / CH waves (latency of one chunk's set-up hidden
+        // behind another's J stores)
+        const long long b = b0 + lane % CH;
+        const bool live = lane < CH && b < P.B;
+        const long long bl = b < P.B ? b : P.B - 1;
         double x0v[5], u[nu];
         const gdouble* x0p = gptr(P.x0) + 5 * bl;
 #pragma unroll
@@ -2435,8 +2444,8 @@ __global__ __launch_bounds__(WAVE, 2) void sweep_kernel(KP Pv)
             for (int k = 0; k <= N; ++k) asm volatile("" : "+v"(CT[k]), "+v"(ST[k]));
 #pragma unroll
             for (int i = 0; i < NO; ++i) asm volatile("" : "+v"(obs[i]));
-            if ((lane >> 5) == h) {
-                double* slot = cfs + (size_t)(lane & (HALF - 1)) * SLOTD;
+            if (lane < CH && lane / QI == h) {
+                double* slot = cfs + (size_t)(lane % QI) * SLOTD;
 #pragma unroll
                 for (int k = 0; k < N; ++k) {
 #pragma unroll
@@ -2478,8 +2487,8 @@ __global__ __launch_bounds__(WAVE, 2) void sweep_kernel(KP Pv)
             wave_sync();
             // ---------------- phase B: the J blocks of this half's instances, one element step s at a time (lane
             // element e = lane + 64 s: row r = e / 5N, column j = e % 5N, the same in every block), 8 blocks per pass
-            const long long bh = b0 + h * HALF;
-            const int cnt = P.B - bh < HALF ? (int)(P.B - bh) : HALF;
+            const long long bh = b0 + h * QI;
+            const int cnt = P.B - bh < QI ? (int)(P.B - bh) : QI;
 #pragma unroll 1
             for (int s = 0; s < S; ++s) {
                 const int e = lane + WAVE * s;
@@ -4109,26 +4118,43 @@ hipError_t launch_lane_f32(int nct, bool modi, const KP& P, hipStream_t st, unsi
 }
 #endif
 
-// sweep kernel (eval hook, N = 3, circles only): one-wave workgroups, a grid-stride over 64-instance chunks on at
-// most the resident workgroups
+// sweep kernel (eval hook, N = 3, circles only): CH-instance chunks per wave, WPG waves per workgroup, a grid-stride
+// over the chunks on at most the resident workgroups
 hipError_t launch_sweep(int nc, bool fen, const KP& P, hipStream_t st);
 #if ALIP_PART_N(3)
-template <int NC, bool FEN>
+template <int NC, bool FEN, int CH, int WPG>
 void launch_sweep_t(const KP& P, hipStream_t st)
 {
-    auto kern = sweep_kernel<NC, FEN>;
-    const size_t smem = SweepL<NC, FEN>::smem;
+    using L = SweepL<NC, FEN>;
+    auto kern = sweep_kernel<NC, FEN, CH, WPG>;
+    const size_t smem = sizeof(double) * ((size_t)L::GL + (size_t)WPG * (CH / 2) * L::SLOTD);
     set_smem((const void*)kern, smem);
-    const unsigned res = resident_blocks((const void*)kern, smem, WAVE);
-    const unsigned need = (unsigned)((P.B + WAVE - 1) / WAVE);
+    const unsigned res = resident_blocks((const void*)kern, smem, WAVE * WPG);
+    const long long per = (long long)CH * WPG;
+    const unsigned need = (unsigned)((P.B + per - 1) / per);
     const unsigned grid = res > 0 && res < need ? res : (need > 0 ? need : 1u);
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(WAVE), smem, st, P);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(WAVE * WPG), smem, st, P);
+}
+template <int NC, bool FEN>
+void launch_sweep_s(const KP& P, hipStream_t st)
+{
+    // instances per wave x waves per workgroup (LDS: the G/E copy per workgroup + CH/2 coefficient slots per
+    // wave); ALIPMPC_SWEEP_SHAPE (dev A/B) picks another shape
+    const char* se = getenv("ALIPMPC_SWEEP_SHAPE");
+    const int shape = se ? atoi(se) : SWEEP_SHAPE_DEFAULT;
+    // measured (profiles/r2/sweep/shapes.txt, B = 65,536): 64 x 1 0.0837 ms (one wave per SIMD: the LDS of a
+    // 64-instance chunk), 32 x 2 0.0759 ms (two per SIMD, 2048 waves), 16 x 4 0.106 ms (232 VGPRs cap the SIMD at
+    // two waves, and each wave repeats the set-up for a quarter of the instances)
+    if (shape == 641)
+        launch_sweep_t<NC, FEN, 64, 1>(P, st);
+    else
+        launch_sweep_t<NC, FEN, 32, 2>(P, st);
 }
 hipError_t launch_sweep(int nc, bool fen, const KP& P, hipStream_t st)
 {
 #define SWCASE(K)                                              \
     case K:                                                    \
-        fen ? launch_sweep_t<K, true>(P, st) : launch_sweep_t<K, false>(P, st); \
+        fen ? launch_sweep_s<K, true>(P, st) : launch_sweep_s<K, false>(P, st); \
         break;
     switch (nc) {
         SWCASE(0) SWCASE(1) SWCASE(2) SWCASE(3) SWCASE(4) SWCASE(5) SWCASE(6)

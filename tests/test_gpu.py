@@ -974,3 +974,23 @@ def test_sweep_kernel_bit_identical_to_group_eval(gpu_lib, variant, nc, B, monke
     s.eval_device(inp, {"J": J})
     torch.cuda.synchronize()
     assert np.array_equal(J.cpu().numpy(), a["J"])
+
+
+@pytest.mark.parametrize("variant,nc,B", [(0, 5, 5003), (1, 3, 4161), (0, 0, 97)])
+def test_sweep_kernel_launch_shapes_bit_identical(gpu_lib, variant, nc, B, monkeypatch):
+    """The sweep kernel's launch shapes (32 instances per wave x 2 waves per workgroup, the default; 64 x 1,
+    ALIPMPC_SWEEP_SHAPE=641) hand instances to lanes differently but run the same per-instance arithmetic: every
+    output bit-equal, on ragged batches (B not a multiple of either chunk) with select_obs / detour on."""
+    from alipmpc import scenes
+    bt = scenes.make_batch_vec(B, seed=41 + nc, n_cir=max(nc, 1), N=3)
+    cir = np.ascontiguousarray(bt["cir"][:, :nc]) if nc else np.zeros((B, 0, 3))
+    ncnt = np.clip(bt["nc"], 0, nc).astype(np.int32)
+    u = bt["u0"] + 0.05 * np.random.default_rng(9).standard_normal(bt["u0"].shape)
+    cfg = gpu_lib.default_cfg(variant, 3, nc_max=nc, ne_max=0)
+    outs = []
+    for shape in (None, "641"):
+        if shape:
+            monkeypatch.setenv("ALIPMPC_SWEEP_SHAPE", shape)
+        outs.append(gpu_lib.Solver(cfg).eval(bt["x0"], bt["goal"], bt["leg"], cir, ncnt, None, None, u))
+    for k in outs[0]:
+        assert np.array_equal(outs[0][k], outs[1][k]), k
