@@ -322,7 +322,7 @@ def timed_loop(step, warmup, K, world, dev):
     return elapsed, ev
 
 
-def jacobian_sweep(alipmpc, scenes, variant, args, dev, reps=10):
+def jacobian_sweep(alipmpc, scenes, variant, args, dev, reps=20):
     """HBM roofline of the unfused Jacobian sweep (the eval hook: f, grad f, c, J of the reference
     callbacks at given u; sweep_kernel at N = 3 with circle slots) on cfg2-shaped instances (N = 3, 5 circles)
     whatever --config is.
@@ -344,22 +344,34 @@ def jacobian_sweep(alipmpc, scenes, variant, args, dev, reps=10):
     st = torch.cuda.current_stream(dev)
     for _ in range(2):
         s.eval_device(inp, out, stream=st)
-    # back-to-back launches (no host sync in between) so the launch latency overlaps the previous kernel;
-    # per-launch HIP events on the launch stream
+    # back-to-back launches (no host sync, no event in between, so each dispatch overlaps the previous kernel)
+    # between one HIP event pair on the launch stream: mean launch duration = elapsed / reps.  An event pair
+    # around every launch adds the ~10 us dispatch of a 65 us kernel (profiles/r2/sweep: rocprofv3 trace 0.0649
+    # ms/launch vs 0.076 ms per-launch events)
     torch.cuda.synchronize(dev)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
-    for a, b in evs:
-        a.record(st)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(st)
+    for _ in range(reps):
         s.eval_device(inp, out, stream=st)
-        b.record(st)
+    b.record(st)
     torch.cuda.synchronize(dev)
-    ms = float(np.mean([a.elapsed_time(b) for a, b in evs[1:]]))
+    ms = a.elapsed_time(b) / reps
     per = 8 * (n + 8 + 3 * cfg.nc_max) + 8 * (1 + n + m + m * n)
     gbs = Bs * per / (ms * 1e-3) / 1e9
-    kern = f"sweep_kernel<{cfg.nc_max},{'true' if variant == alipmpc.VARIANT_MODI else 'false'}>"   # the eval hook at N=3
+    # the eval hook at N = 3 (32 instances per wave, 2 waves per workgroup)
+    kern = f"sweep_kernel<{cfg.nc_max},{'true' if variant == alipmpc.VARIANT_MODI else 'false'},32,2>"
+    # HBM traffic per launch from the committed PMC passes of the same kernel and batch (tools/roofline.py --sweep)
+    traffic = None
+    tp = os.path.join(ROOT, "profiles", "solve_kernel_counters.json")
+    if os.path.exists(tp):
+        try:
+            with open(tp) as fh:
+                traffic = json.load(fh).get(f"{kern}|B={Bs}", {}).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
     return {"kernel": kern, "bound": "hbm", "batch": Bs, "bytes_per_instance": per,
             "kernel_ms": ms, "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
-            "evals_per_s": Bs / (ms * 1e-3)}
+            "traffic": traffic, "evals_per_s": Bs / (ms * 1e-3)}
 
 
 def closed_loop_rate(solver, inp, out, steps, dev, f_cyc=40):

@@ -2,6 +2,7 @@
 """Recompute the bench line's `roofline` fields from a committed profile directory.
 
   python tools/roofline.py profiles/r2/cfg2 [--write profiles/solve_kernel_counters.json]
+  python tools/roofline.py profiles/r2/sweep/r2t --sweep 'sweep_kernel<5,true,32,2>' [--write ...]
 
 The directory holds what tools/gpu_run.sh's `prof` step collects for ONE bench config:
   bench.json                       the bench line of the profiled build (kernel name, B, iterations, peaks)
@@ -53,11 +54,44 @@ def kernel_ms(d, kern):
     return None, 0
 
 
+def sweep(a):
+    """The Jacobian sweep's fields (tools/gpu_sweep_prof.sh: bench.jacobian_sweep alone, no bench.json): HBM bound,
+    algorithmic bytes = bytes_per_instance x B (bench.py's formula), kernel-trace mean duration, PMC traffic."""
+    kname = a.sweep
+    kern = "void alip::" + kname.replace(",", ", ")[:-1]
+    c, meta = counters(a.dir, kern)
+    ms, calls = kernel_ms(a.dir, kern)
+    out = {"kernel": kname, "B": a.batch, "bytes_per_instance": a.bytes, "kernel_ms_trace": ms, "trace_calls": calls}
+    if ms:
+        ach = a.batch * a.bytes / (ms * 1e-3) / 1e9
+        out.update(achieved=ach, peak=8000.0, unit="GB/s", frac=ach / 8000.0)
+    if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+        out["hbm_bytes_per_launch"] = 1024.0 * (2.0 * c["FETCH_SIZE"] + c["WRITE_SIZE"])
+        out["algorithmic_bytes_per_launch"] = a.batch * a.bytes
+        out["fetch_kib"], out["write_kib"] = c["FETCH_SIZE"], c["WRITE_SIZE"]
+    if "GRBM_GUI_ACTIVE" in c and "SQ_INSTS_VALU" in c:
+        out["valu_issue_frac"] = 4.0 * c["SQ_INSTS_VALU"] / (SIMDS * c["GRBM_GUI_ACTIVE"] / XCDS)
+    if "SQ_ACTIVE_INST_ANY" in c and "SQ_WAVE_CYCLES" in c:
+        out["active_issue_frac"] = c["SQ_ACTIVE_INST_ANY"] / c["SQ_WAVE_CYCLES"]
+    out["vgpr"] = meta.get("VGPR_Count") if meta else None
+    print(json.dumps(out, indent=1))
+    if a.write:
+        db = json.load(open(a.write)) if os.path.exists(a.write) else {}
+        db[f"{kname}|B={a.batch}"] = out
+        with open(a.write, "w") as fh:
+            json.dump(db, fh, indent=1)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
     ap.add_argument("--write", default=None, help="merge the counter fields into this JSON (bench.py reads it)")
+    ap.add_argument("--sweep", default=None, help="Jacobian-sweep kernel name, e.g. 'sweep_kernel<5,true,32,2>'")
+    ap.add_argument("--batch", type=int, default=65536)
+    ap.add_argument("--bytes", type=int, default=4272)
     a = ap.parse_args()
+    if a.sweep:
+        return sweep(a)
     bench = json.load(open(os.path.join(a.dir, "bench.json")))
     rl = bench["roofline"]
     kname = rl["kernel"]
