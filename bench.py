@@ -344,12 +344,16 @@ def jacobian_sweep(alipmpc, scenes, variant, args, dev, reps=20):
     st = torch.cuda.current_stream(dev)
     for _ in range(2):
         s.eval_device(inp, out, stream=st)
-    # back-to-back launches (no host sync, no event in between, so each dispatch overlaps the previous kernel)
-    # between one HIP event pair on the launch stream: mean launch duration = elapsed / reps.  An event pair
-    # around every launch adds the ~10 us dispatch of a 65 us kernel (profiles/r2/sweep: rocprofv3 trace 0.0649
-    # ms/launch vs 0.076 ms per-launch events)
+    # back-to-back launches (no host sync, no event in between) between one HIP event pair on the launch stream:
+    # mean launch duration = elapsed / reps.  An event pair around every launch adds the dispatch gap of a 65 us
+    # kernel (profiles/r2/sweep: rocprofv3 trace 0.0649 ms/launch vs 0.076 ms per-launch events)
     torch.cuda.synchronize(dev)
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    # the host enqueues all launches while the stream is held by a spin kernel (one Python + C-ABI call takes about
+    # as long as one 65 us launch: without the hold, the GPU would wait on the host between launches)
+    if hasattr(torch.cuda, "_sleep"):
+        with torch.cuda.stream(st):
+            torch.cuda._sleep(int(2e7))
     a.record(st)
     for _ in range(reps):
         s.eval_device(inp, out, stream=st)

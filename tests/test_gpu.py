@@ -994,3 +994,38 @@ def test_sweep_kernel_launch_shapes_bit_identical(gpu_lib, variant, nc, B, monke
         outs.append(gpu_lib.Solver(cfg).eval(bt["x0"], bt["goal"], bt["leg"], cir, ncnt, None, None, u))
     for k in outs[0]:
         assert np.array_equal(outs[0][k], outs[1][k]), k
+
+
+@pytest.mark.parametrize("program,variant,N,n_cir,n_elp", [
+    ("wave", 0, 3, 5, 0), ("wave", 1, 3, 5, 0), ("wave", 0, 5, 5, 5), ("wave", 2, 3, 5, 0),
+    ("lane", 0, 3, 5, 0), ("lane", 1, 3, 5, 0)])
+@pytest.mark.parametrize("max_iter", [1, 3])
+def test_first_iterates_pin_solve_callbacks(gpu_lib, coracle, program, variant, N, n_cir, n_elp, max_iter):
+    """The solve programs evaluate the NLP with their own row code (wave: row_value / row_coef; lane: row_eval /
+    eval_point; DD: its rollout rows), separate from the eval kernels the g1 goldens pin.  Their first
+    interior-point iterates are a direct check of those callbacks: the Newton step at the reference's warm start
+    is a function of f, grad f, c, J (and the Hessian) there, so u after 1 and 3 iterations must equal the C
+    oracle's (whose callbacks are pinned to the reference, tests/test_oracle.py) to rounding on nearly every
+    instance (Gauss-Jordan vs Cholesky and fma contraction are the only differences)."""
+    from alipmpc import scenes
+    B = 512
+    kw = dict(nc_max=n_cir, ne_max=n_elp, max_iter=max_iter)
+    if program == "lane":
+        kw["program"] = gpu_lib.PROGRAM_LANE
+    s = gpu_lib.Solver(gpu_lib.default_cfg(variant, N, **kw))
+    if variant == 2:   # DD (MPC_DD_sig_step.py): unicycle states, warm start = the last command repeated
+        bt = _dd_batch(B, seed=71 + N, n_cir=n_cir, N=N)
+        o = s.solve(bt["x0"], bt["goal"], None, bt["cir"], bt["nc"], u0=bt["u0"], last_u=bt["last_u"])
+        cc = coracle.default_cfg(2, N, nc_max=n_cir, ne_max=n_elp, max_iter=max_iter)
+        ref = coracle.solve_batch_dd(cc, bt["x0"], bt["goal"], bt["cir"], bt["nc"], None, None, bt["u0"],
+                                     bt["last_u"], nthreads=8)
+    else:
+        bt = scenes.make_batch_vec(B, seed=71 + N + 3 * variant, n_cir=n_cir, n_elp=n_elp, N=N)
+        o = s.solve(bt["x0"], bt["goal"], bt["leg"], bt["cir"], bt["nc"], bt.get("elp"), bt.get("ne"), u0=bt["u0"])
+        ref = _oracle_solve(coracle, dict(variant=variant, N=N, nc_max=n_cir, ne_max=n_elp, max_iter=max_iter), bt)
+    assert np.array_equal(o["iters"] <= max_iter, np.ones(B, bool))
+    scale = np.maximum(1.0, np.abs(ref["u"]))
+    err = (np.abs(o["u"] - ref["u"]) / scale).max(axis=1)
+    assert np.mean(err <= 1e-8) >= 0.99, (np.mean(err <= 1e-8), np.median(err))
+    assert np.median(err) <= 1e-11, np.median(err)
+    assert (o["status"] == ref["status"]).mean() >= 0.99
