@@ -160,6 +160,10 @@ int alipmpc_solve_batch(void* handle, int64_t B,
  * Evaluate the NLP callbacks and the set-up at given u (parity / oracle hook).  m_max = N*rows_per_step.
  *   f B, grad B x n, c B x m_max, J B x m_max x n, cl/cu B x m_max, goal_eff B x 2 (after detour),
  *   row_active B x m_max.  Any output may be NULL.
+ *   Kernels: N = 3 with circle slots only runs the sweep kernel (lane-per-instance set-up, wave-cooperative
+ *   J stores), every other shape eval_kernel; both give the same bits.  Dev knobs (environment):
+ *   ALIPMPC_EVAL_KERNEL=group (read by alipmpc_create) forces eval_kernel, ALIPMPC_SWEEP_SHAPE=641 (read per
+ *   call) the 64-instance sweep shape.
  */
 int alipmpc_eval_batch(void* handle, int64_t B,
                        const double* x0, const double* goal, const int8_t* leg,
