@@ -81,6 +81,8 @@ struct KP {
     const double* last_u;   // DD: previous control (B x 2)
     const uint8_t* active;  // nullable: instances with active[b] == 0 are skipped (closed-loop rollouts)
     uint32_t* queue;        // nullable: work-queue counters of a persistent solve launch (solve_kernel)
+    const int32_t* order;   // nullable: launch order of the wave program (wave / queue slot k solves instance
+                            // order[k]; the closed loop puts last tick's long instances first)
     // solve outputs
     double* u_out;
     double* foot_out;
@@ -1869,13 +1871,20 @@ __global__ __launch_bounds__(256, (solve_waves<KSM, R>())) void solve_kernel(KP 
     __syncthreads();
     const KP& P = *Ps;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);   // wave-uniform (SGPR)
+    // slot k of the launch (wave k, or the k-th queue ticket) solves instance order[k] (identity without an order):
+    // the per-instance arithmetic does not depend on the slot, only when and where the instance runs
     if constexpr (ONE) {
-        const long long b = (long long)blockIdx.x * WAVES_PER_BLOCK + wv;
-        if (b < Pv.B && (!Pv.active || Pv.active[b])) solve_one<N, KSM, R, false>(P, G, E, wsb, wv, b);
+        const long long k = (long long)blockIdx.x * WAVES_PER_BLOCK + wv;
+        if (k < Pv.B) {
+            const long long b = Pv.order ? (long long)__builtin_amdgcn_readfirstlane(Pv.order[k]) : k;
+            if (!Pv.active || Pv.active[b]) solve_one<N, KSM, R, false>(P, G, E, wsb, wv, b);
+        }
     } else {
         uint32_t* const q = Pv.queue;
-        for (long long b = next_instance(q); b < Pv.B; b = next_instance(q))
+        for (long long k = next_instance(q); k < Pv.B; k = next_instance(q)) {
+            const long long b = Pv.order ? (long long)__builtin_amdgcn_readfirstlane(Pv.order[k]) : k;
             if (!Pv.active || Pv.active[b]) solve_one<N, KSM, R, true>(P, G, E, wsb, wv, b);   // rollout: skip finished
+        }
         queue_exit(q);
     }
 }
@@ -3700,6 +3709,38 @@ __global__ __launch_bounds__(256) void cl_project_kernel(CLP C)
     C.sleg[b] = (int8_t)(-C.leg[b]);
 }
 
+// launch order of the next tick's solve (wave program): instances by the iteration count of their last solve,
+// longest first (a counting sort; ties in any order), so the instances that will take longest start first and
+// the launch does not wait on a late-starting long instance (tools/placement.py: cfg2 0.604 -> 0.417 ms with the
+// long instances first).  One workgroup; inactive instances go last.
+constexpr int CL_ORDER_THREADS = 1024;
+__global__ __launch_bounds__(CL_ORDER_THREADS) void cl_order_kernel(const int32_t* iters, const uint8_t* active,
+                                                                    long long B, int32_t* order)
+{
+    constexpr int NK = 64;
+    __shared__ unsigned hist[NK];
+    const int t = threadIdx.x;
+    auto key = [&](long long b) {
+        if (active && !active[b]) return NK - 1;
+        const int it = iters[b];
+        return NK - 2 - (it < 0 ? 0 : (it > NK - 2 ? NK - 2 : it));
+    };
+    if (t < NK) hist[t] = 0u;
+    __syncthreads();
+    for (long long b = t; b < B; b += CL_ORDER_THREADS) atomicAdd(&hist[key(b)], 1u);
+    __syncthreads();
+    if (t == 0) {
+        unsigned acc = 0;
+        for (int k = 0; k < NK; ++k) {
+            const unsigned c = hist[k];
+            hist[k] = acc;
+            acc += c;
+        }
+    }
+    __syncthreads();
+    for (long long b = t; b < B; b += CL_ORDER_THREADS) order[atomicAdd(&hist[key(b)], 1u)] = (int32_t)b;
+}
+
 __global__ __launch_bounds__(256) void cl_update_kernel(CLP C)
 {
     const long long b = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -5006,7 +5047,7 @@ int alipmpc_closed_loop_batch(void* handle, int64_t B, int32_t S, int32_t f_cyc,
             double *x, *pst, *hdv, *mhd, *plan, *xs, *u0, *u, *foot, *xp;
             int8_t *leg, *sleg;
             uint8_t *flags, *act;
-            int32_t *st, *it;
+            int32_t *st, *it, *ord;
             double *goal, *cir, *elp, *ft, *xt, *hd, *actd;
             int32_t *nc, *ne, *stt, *itt, *sg;
             double *vdes, *pose0;
@@ -5017,7 +5058,7 @@ int alipmpc_closed_loop_batch(void* handle, int64_t B, int32_t S, int32_t f_cyc,
         l.u0 = cv.take<double>(Bz * n); l.u = cv.take<double>(Bz * n); l.foot = cv.take<double>(Bz * 3);
         l.xp = cv.take<double>(Bz * n); l.leg = cv.take<int8_t>(Bz); l.sleg = cv.take<int8_t>(Bz);
         l.flags = cv.take<uint8_t>(Bz); l.act = cv.take<uint8_t>(Bz); l.st = cv.take<int32_t>(Bz);
-        l.it = cv.take<int32_t>(Bz);
+        l.it = cv.take<int32_t>(Bz); l.ord = cv.take<int32_t>(Bz);
         if (take_io) {
             l.goal = cv.take<double>(Bz * 2); l.cir = cv.take<double>(Bz * 3 * cf.nc_max);
             l.elp = cv.take<double>(Bz * 5 * cf.ne_max); l.nc = cv.take<int32_t>(Bz); l.ne = cv.take<int32_t>(Bz);
@@ -5092,6 +5133,9 @@ int alipmpc_closed_loop_batch(void* handle, int64_t B, int32_t S, int32_t f_cyc,
     P.goal = d_goal; P.cir = d_cir; P.nc = d_nc; P.elp = d_elp; P.ne = d_ne;
     P.x0 = l.xs; P.leg = l.sleg; P.u0 = l.u0; P.active = l.act;
     P.u_out = l.u; P.foot_out = l.foot; P.x_pred = l.xp; P.status = l.st; P.iters = l.it;
+    // launch ordering (wave program only; ALIPMPC_CL_ORDER=0 turns it off for A/B and the bit-identity test)
+    const char* oe = std::getenv("ALIPMPC_CL_ORDER");
+    const bool order_ok = cf.program != ALIPMPC_PROGRAM_LANE && !(oe && std::strcmp(oe, "0") == 0);
     const int ei = h->evi;
     h->evi = (ei + 1) % Handle::NEV;
     HIPCHK(h, hipEventRecord(h->ev[ei][0], st));
@@ -5105,6 +5149,14 @@ int alipmpc_closed_loop_batch(void* handle, int64_t B, int32_t S, int32_t f_cyc,
             C.bsh_r = std::sinh(beta * rest) * beta; C.tr = rest * (1.0 / T);
             hipLaunchKernelGGL(cl_project_kernel, dim3(g1), dim3(256), 0, st, C);
             HIPCHK(h, hipGetLastError());
+            // wave program: after the first tick, solve last tick's long instances first (same bits per instance)
+            P.order = nullptr;
+            if (order_ok && (s > 0 || i > 0)) {
+                hipLaunchKernelGGL(cl_order_kernel, dim3(1), dim3(CL_ORDER_THREADS), 0, st, (const int32_t*)l.it,
+                                   (const uint8_t*)l.act, (long long)B, l.ord);
+                HIPCHK(h, hipGetLastError());
+                P.order = l.ord;
+            }
             P.queue = h->dq + 2 * (h->qi.fetch_add(1u) % Handle::NQ);
             HIPCHK(h, launch(h, true, P, st));
             hipLaunchKernelGGL(cl_update_kernel, dim3(g1), dim3(256), 0, st, C);

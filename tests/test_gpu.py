@@ -1029,3 +1029,29 @@ def test_first_iterates_pin_solve_callbacks(gpu_lib, coracle, program, variant, 
     assert np.mean(err <= 1e-8) >= 0.99, (np.mean(err <= 1e-8), np.median(err))
     assert np.median(err) <= 1e-11, np.median(err)
     assert (o["status"] == ref["status"]).mean() >= 0.99
+
+
+@pytest.mark.parametrize("variant,kick", [(0, 0.0), (1, 0.05)])
+def test_closed_loop_launch_order_bit_identical(gpu_lib, variant, kick, monkeypatch):
+    """The closed loop launches each tick's solves longest-first (by the last tick's iteration counts; a counting
+    sort whose ties fall in any order).  The order changes when and on which SIMD an instance runs, never its
+    arithmetic: every output equals the identity-order loop's (ALIPMPC_CL_ORDER=0) bit for bit, on a batch above
+    one wave per SIMD's worth of instances with stops, kicks and infeasible scenes."""
+    from alipmpc import scenes
+    B, S, F = 3000, 2, 40
+    bt = scenes.make_batch(B, seed=610 + variant, n_cir=5)
+    x0 = bt["x0"].copy()
+    x0[:300, 0:2] = bt["goal"][:300] - np.array([0.6, 0.5])
+    leg = bt["leg"].astype(np.int8)
+    cfg = gpu_lib.default_cfg(variant, 3, nc_max=5, ne_max=0)
+    s0 = gpu_lib.Solver(cfg)
+    foot0 = s0.solve(x0, bt["goal"], leg, bt["cir"], bt["nc"], u0=np.tile(x0, (1, 3)))["foot"][:, 0:2]
+    outs = []
+    for order in ("1", "0"):
+        monkeypatch.setenv("ALIPMPC_CL_ORDER", order)
+        outs.append(gpu_lib.Solver(cfg).closed_loop(x0, foot0, bt["goal"], leg, bt["cir"], bt["nc"], steps=S, f_cyc=F,
+                                                    kick=kick, seed=3))
+    a, b = outs
+    assert (a["status"] == 2).sum() > 0 and (a["steps_to_goal"] > 0).sum() > 0
+    for k in a:
+        assert np.array_equal(a[k], b[k], equal_nan=True), k
