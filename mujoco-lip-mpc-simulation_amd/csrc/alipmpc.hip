@@ -3741,6 +3741,45 @@ __global__ __launch_bounds__(CL_ORDER_THREADS) void cl_order_kernel(const int32_
     for (long long b = t; b < B; b += CL_ORDER_THREADS) order[atomicAdd(&hist[key(b)], 1u)] = (int32_t)b;
 }
 
+// launch order of a cold solve (wave program): instances by the number of rows the warm start violates (the eval
+// hook's c / cl / cu / activity at u0), most first — a cheap predictor of the long instances (cfg2: 319 of the
+// 479 instances that take >= 25 iterations are in the top 958), so they start first.  One workgroup, a counting
+// sort (ties in any order); only the order changes, never an instance's arithmetic.
+constexpr int SOLVE_ORDER_MAX_B = 8192;   // cold-solve ordering for batches up to this size (one workgroup's LDS keys)
+__global__ __launch_bounds__(CL_ORDER_THREADS) void solve_order_kernel(const double* c, const double* cl, const double* cu,
+                                                                      const int8_t* act, int m, long long B, int32_t* order)
+{
+    constexpr int NK = 64;
+    __shared__ unsigned hist[NK];
+    __shared__ unsigned char keys[SOLVE_ORDER_MAX_B];
+    const int t = threadIdx.x;
+    auto key = [&](long long b) { return (int)keys[b]; };
+    if (t < NK) hist[t] = 0u;
+    // key = NK - 1 - (violated rows of the instance), computed once into LDS
+    for (long long b = t; b < B; b += CL_ORDER_THREADS) {
+        int v = 0;
+        for (int r = 0; r < m; ++r) {
+            const size_t o = (size_t)b * m + r;
+            const double cv = c[o];
+            v += (act[o] && (cv < cl[o] - 1e-6 || cv > cu[o] + 1e-6)) ? 1 : 0;
+        }
+        keys[b] = (unsigned char)(NK - 1 - (v > NK - 1 ? NK - 1 : v));
+    }
+    __syncthreads();
+    for (long long b = t; b < B; b += CL_ORDER_THREADS) atomicAdd(&hist[key(b)], 1u);
+    __syncthreads();
+    if (t == 0) {
+        unsigned acc = 0;
+        for (int k = 0; k < NK; ++k) {
+            const unsigned cnt = hist[k];
+            hist[k] = acc;
+            acc += cnt;
+        }
+    }
+    __syncthreads();
+    for (long long b = t; b < B; b += CL_ORDER_THREADS) order[atomicAdd(&hist[key(b)], 1u)] = (int32_t)b;
+}
+
 __global__ __launch_bounds__(256) void cl_update_kernel(CLP C)
 {
     const long long b = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -4244,6 +4283,9 @@ struct Handle {
     // rollout working set (evolving state, warm starts, per-step solve outputs)
     void* rstage = nullptr;
     size_t rstage_bytes = 0;
+    // cold-solve launch order: the eval hook's outputs at the warm start and the order (launch_solve_ordered)
+    void* ostage = nullptr;
+    size_t ostage_bytes = 0;
     hipStream_t own = nullptr;
     // launch timing: a ring of event pairs, so a re-record never targets an event still pending on the
     // stream (that serialises the host with the previous launch)
@@ -4746,6 +4788,42 @@ int alipmpc_create(const alipmpc_cfg* cfg, int device, void** handle)
     return ALIPMPC_OK;
 }
 
+// a solve launch of the wave program (cold solves of up to SOLVE_ORDER_MAX_B instances): the eval hook at the warm
+// start, solve_order_kernel, then the solve in that order — the instances predicted long start first.  Opt-in
+// (ALIPMPC_SOLVE_ORDER=1) until measured on the bench config; per-instance results are the same bits either way.
+static hipError_t launch_solve_ordered(Handle* h, KP P, hipStream_t st)
+{
+    const alipmpc_cfg& cf = h->cfg;
+    const char* oe = std::getenv("ALIPMPC_SOLVE_ORDER");
+    if (cf.variant == ALIPMPC_VARIANT_DD || cf.program == ALIPMPC_PROGRAM_LANE || P.order || P.B < 2 ||
+        P.B > SOLVE_ORDER_MAX_B || !P.u0 || !(oe && std::strcmp(oe, "1") == 0))
+        return launch(h, true, P, st);
+    const size_t Bz = (size_t)P.B, m = (size_t)h->m_max;
+    const size_t need = Bz * m * 8 * 3 + Bz * 4 + Bz * m + 256;
+    if (h->ostage_bytes < need) {
+        if (h->ostage) (void)hipFree(h->ostage);
+        h->ostage = nullptr;
+        h->ostage_bytes = 0;
+        if (hipError_t e = hipMalloc(&h->ostage, need)) return e;
+        h->ostage_bytes = need;
+    }
+    double* c = (double*)h->ostage;
+    double* cl = c + Bz * m;
+    double* cu = cl + Bz * m;
+    int32_t* ord = (int32_t*)(cu + Bz * m);
+    int8_t* act = (int8_t*)(ord + Bz);
+    KP E = make_kp(h, P.B, false);
+    E.x0 = P.x0; E.goal = P.goal; E.leg = P.leg; E.cir = P.cir; E.nc = P.nc; E.elp = P.elp; E.ne = P.ne;
+    E.u0 = P.u0; E.last_u = P.last_u;
+    E.c_out = c; E.cl_out = cl; E.cu_out = cu; E.active_out = act;
+    if (hipError_t e = launch(h, false, E, st)) return e;
+    hipLaunchKernelGGL(solve_order_kernel, dim3(1), dim3(CL_ORDER_THREADS), 0, st, (const double*)c, (const double*)cl,
+                       (const double*)cu, (const int8_t*)act, (int)m, (long long)P.B, ord);
+    if (hipError_t e = hipGetLastError()) return e;
+    P.order = ord;
+    return launch(h, true, P, st);
+}
+
 static int run_batch(Handle* h, bool solve, int64_t B, const double* x0, const double* goal, const int8_t* leg,
                      const double* cir, const int32_t* nc, const double* elp, const int32_t* ne, const double* u0,
                      const double* last_u, double* u_out, double* foot_out, double* x_pred, int32_t* status, int32_t* iters, double* f,
@@ -4776,7 +4854,7 @@ static int run_batch(Handle* h, bool solve, int64_t B, const double* x0, const d
         const int ei = h->evi;
         h->evi = (ei + 1) % Handle::NEV;
         HIPCHK(h, hipEventRecord(h->ev[ei][0], st));
-        HIPCHK(h, launch(h, solve, P, st));
+        HIPCHK(h, solve ? launch_solve_ordered(h, P, st) : launch(h, false, P, st));
         HIPCHK(h, hipEventRecord(h->ev[ei][1], st));
         h->evlast = ei;
         h->timed = true;
@@ -4858,7 +4936,7 @@ static int run_batch(Handle* h, bool solve, int64_t B, const double* x0, const d
     const int ei = h->evi;
     h->evi = (ei + 1) % Handle::NEV;
     HIPCHK(h, hipEventRecord(h->ev[ei][0], st));
-    HIPCHK(h, launch(h, solve, P, st));
+    HIPCHK(h, solve ? launch_solve_ordered(h, P, st) : launch(h, false, P, st));
     HIPCHK(h, hipEventRecord(h->ev[ei][1], st));
     h->evlast = ei;
     h->timed = true;
@@ -5371,6 +5449,7 @@ void alipmpc_destroy(void* handle)
     if (h->dlk) hipFree(h->dlk);
     if (h->dlkf) hipFree(h->dlkf);
     if (h->stage) hipFree(h->stage);
+    if (h->ostage) hipFree(h->ostage);
     if (h->rstage) hipFree(h->rstage);
     for (auto& pr : h->ev)
         for (hipEvent_t e : pr)
