@@ -50,3 +50,16 @@ for t in range(40):
     chain["u0"].copy_(out["u"])
 print("chained warm x40 ms:", np.round(ds, 3))
 print("chained warm x40 iters:", its)
+# enqueued without host syncs (as alipmpc_closed_loop_batch does): solves alone, then solves interleaved with a
+# tiny kernel that uses no scratch (the closed loop's project / update kernels stand in)
+tiny = torch.zeros(4096, dtype=torch.float64, device=dev)
+for inter in (False, True, False):
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(40)]
+    for a, b in ev:
+        if inter:
+            tiny.add_(1.0)
+        a.record(st); s.solve_device(inp, out, stream=st); b.record(st)
+        if inter:
+            tiny.mul_(0.5)
+    torch.cuda.synchronize()
+    print("interleaved" if inter else "alone      ", np.round([a.elapsed_time(b) for a, b in ev], 2))
