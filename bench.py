@@ -7,7 +7,8 @@ One "step" = one fused interior-point solve of a batch of B independent NLP inst
 already resident in HBM (one launch of solve_kernel through the C ABI on the current HIP stream).
 Default workload = BASELINE configs[1] ("cfg2"): B = 4096 random ALIP initial states per GPU, N = 3,
 5 circular obstacles, fp64.  For N > 1 GPUs (torchrun, one process per GPU, RCCL) every rank solves its
-own shard (scenes are generated from (seed, rank)) and each step ends with one RCCL gather of the
+own shard (instances are generated from (seed, global index), so every GPU count solves the same instances
+with the same program) and each step ends with one RCCL gather of the
 per-instance outputs to rank 0 — the path has no other exchange.
 The other BASELINE configs are presets (not the driver's default line):
   cfg1  B = 1, N = 3, no obstacles, sig_step (the reference's own CPU-runnable case: single-solve latency)
@@ -37,19 +38,23 @@ FP32_PEAK_TFLOPS = 157.3     # MI355X FP32 matrix = vector peak (MI355X_MICROARC
 
 # BASELINE.json configs: (instances, per_gpu?, horizon, circles, ellipses, precision, distinct fields).
 # program: the device program (cfg.program, include/alipmpc.h) — "wave" (one instance per wavefront: the
-# latency-bound small batches: cfg1, cfg2, and cfg4's 32k-instance shards at 8 GPUs), "lane" (one instance
-# per lane: batches of 10^5+ instances per GPU; N = 3 circles only), "auto" = lane when the rank's shard
-# has at least LANE_MIN_B instances (the measured crossover, profiles/r2/) and the shape allows it.
+# latency-bound small batches: cfg1, cfg2; cfg3, whose N = 5 ellipse shape the lane program does not cover), "lane"
+# (one instance per lane: the 10^5+-instance configs cfg4 / cfg5).  A property of the config, never of the shard
+# size: every GPU count runs the same program on the same instances, so the outputs do not depend on world size.
 CONFIGS = {
     "cfg1": dict(batch=1, per_gpu=True, horizon=3, circles=0, ellipses=0, fp32=False, variant="sig_step",
                  program="wave"),
     "cfg2": dict(batch=4096, per_gpu=True, horizon=3, circles=5, ellipses=0, fp32=False, program="wave"),
     "cfg3": dict(batch=65536, per_gpu=True, horizon=5, circles=5, ellipses=5, fp32=False, program="wave"),
-    "cfg4": dict(batch=262144, per_gpu=False, horizon=3, circles=5, ellipses=0, fp32=False, program="auto"),
-    "cfg5": dict(batch=1048576, per_gpu=False, horizon=3, circles=5, ellipses=0, fp32=True, program="auto"),
+    "cfg4": dict(batch=262144, per_gpu=False, horizon=3, circles=5, ellipses=0, fp32=False, program="lane"),
+    "cfg5": dict(batch=1048576, per_gpu=False, horizon=3, circles=5, ellipses=0, fp32=True, program="lane"),
 }
-LANE_MIN_B = 65536
 HBM_PEAK_GBS = 8000.0
+# scene blocks: instance g of a config's global batch is instance g % BLOCK of block g // BLOCK, generated from
+# (seed * 1000 + g // BLOCK) — so a shard [lo, hi) holds the same instances whatever the world size (SURVEY 8e:
+# scenes from (seed, global index)).  Per-GPU (weak-scaling) configs use blocks of the per-rank batch: rank r's shard
+# is block r (the seed recipe of rounds 1-2, seed * 1000 + rank).
+BLOCK = {"cfg4": 32768, "cfg5": 32768}
 
 
 def flops_per_iter(n, m, N, nobs):
@@ -62,6 +67,38 @@ def flops_per_iter(n, m, N, nobs):
 def solve_rows(N, rps, modi):
     """Constraint rows of the solve layout (f_en split into two rows for modi)."""
     return N * (rps + (1 if modi else 0))
+
+
+def scene_block(config, k, size, seed, n_cir, n_elp, N):
+    """Block k of a config's global instance sequence (SURVEY 8d distribution; seed * 1000 + k)."""
+    from alipmpc import scenes
+    s = seed * 1000 + k
+    if config == "cfg2":
+        return scenes.make_batch(size, seed=s, n_cir=n_cir, N=N)
+    # vectorised generator: one obstacle field per instance (cfg3: 4096 fields shared within a block)
+    return scenes.make_batch_vec(size, seed=s, n_cir=n_cir, n_elp=n_elp, N=N, fields=4096 if config == "cfg3" else None)
+
+
+def global_inputs(config, lo, hi, block, seed, n_cir, n_elp, N):
+    """Instances [lo, hi) of the global batch: the blocks they overlap, generated from (seed, block index) and
+    sliced, so the same global index always holds the same instance.  ALIPMPC_SCENE_CACHE=<dir> keeps the arrays
+    between runs of one profiling session (tools/gpu_run.sh prof: cfg5 takes ~45 s to generate)."""
+    cache = os.environ.get("ALIPMPC_SCENE_CACHE")
+    if cache:
+        fn = os.path.join(cache, f"{config}_{lo}_{hi}_{block}_{seed}_{n_cir}_{n_elp}_{N}.npz")
+        if os.path.exists(fn):
+            with np.load(fn) as z:
+                return {k: z[k] for k in z.files}
+    parts = []
+    for k in range(lo // block, (hi - 1) // block + 1):
+        bt = scene_block(config, k, block, seed, n_cir, n_elp, N)
+        a, b = max(lo, k * block) - k * block, min(hi, (k + 1) * block) - k * block
+        parts.append({key: v[a:b] for key, v in bt.items() if v is not None})
+    out = {key: np.concatenate([p[key] for p in parts]) for key in parts[0]}
+    if cache:
+        os.makedirs(cache, exist_ok=True)
+        np.savez(fn, **out)
+    return out
 
 
 def parse():
@@ -80,7 +117,7 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")),
                     help="threads for the all-cores CPU baseline (the GPU box allots 16)")
     ap.add_argument("--sweep-batch", type=int, default=65536, help="instances for the Jacobian-sweep roofline")
-    ap.add_argument("--program", default=None, choices=["wave", "lane", "auto"], help="default: the config's")
+    ap.add_argument("--program", default=None, choices=["wave", "lane"], help="default: the config's")
     ap.add_argument("--closed-loop-steps", type=int, default=1,
                     help="walking steps of the per-tick closed-loop figure (f_cyc = 40 solves each; 0 = skip)")
     return ap.parse_args()
@@ -120,18 +157,15 @@ def main():
         B = hi - lo
     prec = {"precision": alipmpc.PREC_FP32} if fp32 else {}
     program = args.program or preset.get("program", "wave")
-    lane_ok = N == 3 and n_elp == 0 and n_cir <= 6
-    if program == "auto":
-        program = "lane" if (lane_ok and B >= LANE_MIN_B) else "wave"
     prec["program"] = alipmpc.PROGRAM_LANE if program == "lane" else alipmpc.PROGRAM_WAVE
     cfg = alipmpc.default_cfg(variant, N, nc_max=n_cir, ne_max=n_elp, **prec)
     solver = alipmpc.Solver(cfg, device=dev.index)
-    seed = args.seed * 1000 + rank
-    if args.config == "cfg2":
-        batch = scenes.make_batch(B, seed=seed, n_cir=n_cir, N=N)
-    else:   # vectorised generator: one obstacle field per instance (cfg3: 4096 shared fields)
-        batch = scenes.make_batch_vec(B, seed=seed, n_cir=n_cir, n_elp=n_elp, N=N,
-                                      fields=4096 if args.config == "cfg3" else None)
+    weak = preset["per_gpu"] or args.batch is not None
+    if weak:     # rank r's shard = block r of the global sequence
+        block, lo = B, rank * B
+    else:
+        block, lo = BLOCK[args.config], sharding_lo(preset["batch"], rank, world)
+    batch = global_inputs(args.config, lo, lo + B, block, args.seed, n_cir, n_elp, N)
     n = solver.n
     inp = {
         "x0": torch.from_numpy(batch["x0"]).to(dev),
@@ -180,14 +214,8 @@ def main():
     # counter-derived fields of the dominant kernel from the committed rocprofv3 passes of this config
     # (tools/roofline.py writes profiles/solve_kernel_counters.json from profiles/r2/<config>/): HBM traffic and
     # the issue / MFMA shares that say which bound the kernel actually sits against
-    prof = {}
-    tp = os.path.join(ROOT, "profiles", "solve_kernel_counters.json")
-    if os.path.exists(tp):
-        try:
-            with open(tp) as fh:
-                prof = json.load(fh).get(f"{kname}|B={B}", {})
-        except Exception:
-            prof = {}
+    bid = alipmpc.build_id()
+    prof = counter_record(f"{kname}|B={B}", bid)
     traffic = prof.get("hbm_bytes_per_launch")
 
     # quality beside the rate (every config): solves/s counts every instance, so report how many of them
@@ -201,8 +229,10 @@ def main():
     cpu = cpu_mt = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(cfg, batch, args.cpu_seconds, workload=args.config)
-        # the same C restatement with OpenMP over the host cores this job may use
-        cpu_mt = cpu_baseline(cfg, batch, args.cpu_seconds / 2, threads=args.cpu_threads, workload=args.config)
+        # the same C restatement with OpenMP over the host cores this job may use (batches that give
+        # every thread at least one 64-instance chunk)
+        if B >= 64 * args.cpu_threads:
+            cpu_mt = cpu_baseline(cfg, batch, args.cpu_seconds / 2, threads=args.cpu_threads, workload=args.config)
 
     if rank == 0:
         line = {
@@ -217,7 +247,8 @@ def main():
             "scaling": "weak" if preset["per_gpu"] or args.batch is not None else "strong",
             "vs_baseline": None,
             "dtype": "f32" if fp32 else "f64",
-            "data": "synthetic (rand_obs distribution, SURVEY 8d), generated per rank from (seed, rank)",
+            "data": f"synthetic (rand_obs distribution, SURVEY 8d), instances generated from (seed, global index) in "
+                    f"blocks of {block}",
             "config": {
                 "workload": f"{args.config}: {B_total} ALIP initial states ({B} on rank 0), N={N} horizon, "
                             f"{n_cir} circles + {n_elp} ellipses, variant={args.variant}, "
@@ -230,7 +261,9 @@ def main():
                 "resident_slots": slots,
                 "program": program,
                 "launch": ("persistent work queue, one instance per lane" if program == "lane" else
+                           "one wavefront per instance (B <= resident slots, no queue)" if slots and B <= slots else
                            "persistent work queue, one instance per wavefront"),
+                "build_id": bid,
             },
             "roofline": {
                 "kernel": kname,
@@ -244,7 +277,7 @@ def main():
                 "active_issue_frac": prof.get("active_issue_frac"),
                 "mfma_busy_share": prof.get("mfma_busy_share"),
                 "insts_per_iter": prof.get("insts_per_iter"),
-                "counters": "profiles/solve_kernel_counters.json (tools/roofline.py)" if prof else None,
+                "counters": ("profiles/solve_kernel_counters.json (tools/roofline.py), build " + bid) if prof else None,
                 "kernel_ms": kernel_ms,
                 "flops_per_iter": fpi,
                 "iters_per_launch": int(iters.sum()),
@@ -258,6 +291,11 @@ def main():
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()
+
+
+def sharding_lo(total, rank, world):
+    from alipmpc import sharding
+    return sharding.shard_range(total, rank, world)[0]
 
 
 def B_total_of(preset, args, B, world):
@@ -322,6 +360,18 @@ def timed_loop(step, warmup, K, world, dev):
     return elapsed, ev
 
 
+def counter_record(key, bid):
+    """The committed rocprofv3 counter record of kernel|B (profiles/solve_kernel_counters.json, tools/roofline.py) —
+    only when it was measured on this very build (same alipmpc_build_id); otherwise none, never a stale one."""
+    tp = os.path.join(ROOT, "profiles", "solve_kernel_counters.json")
+    try:
+        with open(tp) as fh:
+            rec = json.load(fh).get(key, {})
+    except (OSError, ValueError):
+        return {}
+    return rec if rec.get("build_id") == bid else {}
+
+
 def jacobian_sweep(alipmpc, scenes, variant, args, dev, reps=20):
     """HBM roofline of the unfused Jacobian sweep (the eval hook: f, grad f, c, J of the reference
     callbacks at given u; sweep_kernel at N = 3 with circle slots) on cfg2-shaped instances (N = 3, 5 circles)
@@ -365,14 +415,7 @@ def jacobian_sweep(alipmpc, scenes, variant, args, dev, reps=20):
     # the eval hook at N = 3 (32 instances per wave, 2 waves per workgroup)
     kern = f"sweep_kernel<{cfg.nc_max},{'true' if variant == alipmpc.VARIANT_MODI else 'false'},32,2>"
     # HBM traffic per launch from the committed PMC passes of the same kernel and batch (tools/roofline.py --sweep)
-    traffic = None
-    tp = os.path.join(ROOT, "profiles", "solve_kernel_counters.json")
-    if os.path.exists(tp):
-        try:
-            with open(tp) as fh:
-                traffic = json.load(fh).get(f"{kern}|B={Bs}", {}).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    traffic = counter_record(f"{kern}|B={Bs}", alipmpc.build_id()).get("hbm_bytes_per_launch")
     return {"kernel": kern, "bound": "hbm", "batch": Bs, "bytes_per_instance": per,
             "kernel_ms": ms, "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
             "traffic": traffic, "evals_per_s": Bs / (ms * 1e-3)}
@@ -471,9 +514,10 @@ def cpu_baseline(cfg, batch, seconds, threads=1, workload="cfg2"):
                       nthreads=threads)
         done += i1 - i0
     dt = time.perf_counter() - t0
+    prec = " (fp64: the GPU line runs fp32)" if cfg.precision == 1 else ""
     return {"value": done / dt, "unit": "solves/s", "cores": threads, "kind": "port",
             "sample": f"{done} instances of the {workload} workload (first {min(done, B)} of the GPU batch, cycled), "
-                      f"C oracle oracle/alipmpc_oracle.c, same interior-point algorithm, {threads} thread(s), "
+                      f"C oracle oracle/alipmpc_oracle.c, same interior-point algorithm{prec}, {threads} thread(s), "
                       f"{dt:.1f} s"}
 
 

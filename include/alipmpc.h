@@ -284,6 +284,11 @@ const char* alipmpc_solve_program(void* handle);
  * events on the launch stream (0 if none). */
 double alipmpc_last_kernel_ms(void* handle);
 
+/* Identifier of this library build: 16 hex digits of a sha256 over the sources and compile flags it was built from
+ * (alipmpc/build.py).  Profiles and counter records carry it, so tools never attach one build's counters to another
+ * build's measurement.  No reference counterpart. */
+const char* alipmpc_build_id(void);
+
 const char* alipmpc_last_error(void* handle);
 void alipmpc_destroy(void* handle);
 

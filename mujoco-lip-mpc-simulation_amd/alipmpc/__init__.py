@@ -4,12 +4,12 @@
   default_cfg  the reference's constants per variant (modi / sig_step / dd)
   planner      MPCCBF drop-in (reference MPC_LIP_modi.MPCCBF signatures) + solve_batch
 """
-from ._lib import (Cfg, Solver, default_cfg, load, lib_path, num_vars, rows_per_step, trace_len, EXPORTS, STATUS_NAMES,
+from ._lib import (Cfg, Solver, default_cfg, load, lib_path, build_id, num_vars, rows_per_step, trace_len, EXPORTS, STATUS_NAMES,
                    VARIANT_MODI, VARIANT_SIG_STEP, VARIANT_DD, PREC_FP64, PREC_FP32, PROGRAM_WAVE, PROGRAM_LANE,
                    ROLLOUT_DONE, FP32_TOL,
                    FP32_ACCEPTABLE_TOL, FP32_TOL_LONG, FP32_ACCEPTABLE_TOL_LONG)
 
-__all__ = ["Cfg", "Solver", "default_cfg", "load", "lib_path", "num_vars", "rows_per_step", "trace_len", "EXPORTS",
+__all__ = ["Cfg", "Solver", "default_cfg", "load", "lib_path", "build_id", "num_vars", "rows_per_step", "trace_len", "EXPORTS",
            "STATUS_NAMES", "VARIANT_MODI", "VARIANT_SIG_STEP", "VARIANT_DD", "PREC_FP64", "PREC_FP32",
            "PROGRAM_WAVE", "PROGRAM_LANE", "ROLLOUT_DONE", "FP32_TOL", "FP32_ACCEPTABLE_TOL",
            "FP32_TOL_LONG", "FP32_ACCEPTABLE_TOL_LONG"]

@@ -41,6 +41,7 @@ EXPORTS = ("alipmpc_default_cfg", "alipmpc_rows_per_step", "alipmpc_num_vars", "
            "alipmpc_solve_batch", "alipmpc_eval_batch", "alipmpc_rollout_batch", "alipmpc_closed_loop_batch",
            "alipmpc_trace_len",
            "alipmpc_trace_batch", "alipmpc_nominal_gait_batch", "alipmpc_solve_slots", "alipmpc_solve_program", "alipmpc_last_kernel_ms",
+           "alipmpc_build_id",
            "alipmpc_last_error", "alipmpc_destroy")
 
 _lib = None
@@ -48,6 +49,12 @@ _lib = None
 
 def lib_path():
     return _build.LIB
+
+
+def build_id():
+    """The loaded library's build id (include/alipmpc.h: alipmpc_build_id; "unknown" for builds without one)."""
+    L = load()
+    return L.alipmpc_build_id().decode() if hasattr(L, "alipmpc_build_id") else "unknown"
 
 
 def load(build_if_missing=True):
@@ -94,6 +101,9 @@ def load(build_if_missing=True):
     if hasattr(L, "alipmpc_solve_program"):
         L.alipmpc_solve_program.argtypes = [P]
         L.alipmpc_solve_program.restype = ctypes.c_char_p
+    if hasattr(L, "alipmpc_build_id"):
+        L.alipmpc_build_id.argtypes = []
+        L.alipmpc_build_id.restype = ctypes.c_char_p
     L.alipmpc_last_kernel_ms.argtypes = [P]
     L.alipmpc_last_kernel_ms.restype = ctypes.c_double
     L.alipmpc_last_error.argtypes = [P]

@@ -6,6 +6,7 @@ csrc/alipmpc.hip is compiled as 9 translation units in parallel — ALIP_PART=0 
 kernels), ALIP_PART=1..6 (the solve/eval kernels of one horizon N each, fp64 and fp32) and ALIP_PART=7/8 (the
 lane solver of csrc/lane_solve.inc, fp64 / fp32) — and linked into one shared library.  `ALIPMPC_SINGLE_TU=1` builds it as one TU instead (slower, same code).
 """
+import hashlib
 import os
 import subprocess
 import sys
@@ -31,6 +32,18 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC",
          "-Wno-unused-value"]
 
 
+def build_id(extra=(), src=None):
+    """16-hex id of a build: sha256 over the sources it compiles (kernel sources, the header, this file's flags)
+    and the extra flags.  Compiled into the library (alipmpc_build_id) so a counter record made with one build is
+    never attached to a bench line of another (tools/roofline.py, bench.py)."""
+    h = hashlib.sha256()
+    for p in (src or SRC, INC, MATH, HDR):
+        with open(p, "rb") as fh:
+            h.update(fh.read())
+    h.update(" ".join([*ARCH, *FLAGS, *extra]).encode())
+    return h.hexdigest()[:16]
+
+
 def needs_build():
     if not os.path.exists(LIB):
         return True
@@ -51,6 +64,7 @@ def build(force=False, verbose=True, extra=(), out=None, src=None):
     if not force and out is None and not needs_build():
         return LIB
     tmp_lib = target + ".tmp"
+    extra = [*extra, f'-DALIP_BUILD_ID="{build_id(extra, src)}"']
     if os.environ.get("ALIPMPC_SINGLE_TU") == "1":
         _run([HIPCC, *ARCH, *FLAGS, *extra, "-shared", "-o", tmp_lib, src], verbose)
     else:

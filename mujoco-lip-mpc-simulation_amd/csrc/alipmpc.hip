@@ -133,6 +133,39 @@ __device__ unsigned long long g_stamps[NSTAMP];
 #define STAMP_FLUSH do {} while (0)
 #endif
 
+// ---- diagnostic per-instance record of the wave program (compiled only with -DALIP_WSTAMP; never in the product
+// build): [start, end] of the instance on the constant 100 MHz clock and the shader clock, HW_ID / XCC_ID of the wave,
+// iterations, line-search trials, restorations.  Slot = g_wstamp_base + instance (the closed loop sets the base per
+// tick), 8 values per slot, written by lanes 0..7 (vector stores).  tools/cl_wstamps.py reads it.
+#ifdef ALIP_WSTAMP
+constexpr long long WSTAMP_CAP = 48 * 4096;
+__device__ unsigned long long g_wstamp[WSTAMP_CAP * 8];
+__device__ long long g_wstamp_base;
+#define WSTAMP_DECL                                                                        \
+    const unsigned long long ws_t0 = __builtin_amdgcn_s_memrealtime();                    \
+    const unsigned long long ws_c0 = __builtin_amdgcn_s_memtime();                        \
+    unsigned ws_trials = 0;
+#define WSTAMP_TRIAL ++ws_trials
+#define WSTAMP_WRITE(b, it, nrest)                                                         \
+    do {                                                                                   \
+        const unsigned long long t1_ = __builtin_amdgcn_s_memrealtime();                   \
+        const unsigned long long c1_ = __builtin_amdgcn_s_memtime();                       \
+        const unsigned hw_ = __builtin_amdgcn_s_getreg(4 | (31 << 11));                   \
+        const unsigned xcc_ = __builtin_amdgcn_s_getreg(20 | (15 << 11));                 \
+        const long long slot_ = g_wstamp_base + (b);                                       \
+        const int l_ = lane_id();                                                          \
+        unsigned long long v_ = l_ == 0 ? ws_t0 : l_ == 1 ? t1_ : l_ == 2 ? ws_c0 : l_ == 3 ? c1_ \
+                              : l_ == 4 ? ((unsigned long long)xcc_ << 32 | hw_)                \
+                              : l_ == 5 ? (unsigned long long)(it) : l_ == 6 ? (unsigned long long)ws_trials \
+                              : (unsigned long long)(nrest);                               \
+        if (slot_ >= 0 && slot_ < WSTAMP_CAP && l_ < 8) g_wstamp[slot_ * 8 + l_] = v_;     \
+    } while (0)
+#else
+#define WSTAMP_DECL
+#define WSTAMP_TRIAL do {} while (0)
+#define WSTAMP_WRITE(b, it, nrest) do {} while (0)
+#endif
+
 template <int N>
 struct Dim {
     static constexpr int n = 3 * N;     // decision = footholds p_0..p_{N-1} (see build_tables)
@@ -1102,6 +1135,7 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
     const int mr4 = rfl(P.mr4), mo4 = rfl(P.mo4), m_max = rfl(P.m_max), rps = rfl(P.rps);
     const int nc_max = rfl(P.nc_max), ne_max = rfl(P.ne_max), nobs = nc_max + ne_max;
     const int modi = rfl(P.modi), max_iter = rfl(P.max_iter);
+    WSTAMP_DECL
     WSS<N, R> w = carve_s<N, R>(wsb + (size_t)wv * wss_elems<N, R>(nc_max, ne_max, mr4, mo4), nc_max, ne_max, mr4, mo4);
     for (int i = lane; i < 64 * (N + 1); i += WAVE) w.S[i] = R(0.0);
 
@@ -1616,6 +1650,7 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
         R ctr[RPL], ta0[RPL], ta1[RPL];
         R ft = R(0.0), lgt = R(0.0), tht_acc = R(0.0);
         while (a >= amin) {
+            WSTAMP_TRIAL;
             RELANE();
             R tht = R(0.0);
             ft = R(0.0);
@@ -1794,6 +1829,7 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
         else if (viol > R(1e-4))
             status = 2;
     }
+    WSTAMP_WRITE(b, it, n_rest);
     // canonical u: u_k = x_{k+1} (W u_k = p_k since W B = I) — the reference's "desired next state"
     if (lane < 5 * N) P.u_out[(size_t)b * 5 * N + lane] = w.V[gx(lane / 5 + 1, lane % 5)];
     if (P.foot_out && lane < 3) P.foot_out[3 * b + lane] = w.V[gp(0, lane)];
@@ -3741,45 +3777,6 @@ __global__ __launch_bounds__(CL_ORDER_THREADS) void cl_order_kernel(const int32_
     for (long long b = t; b < B; b += CL_ORDER_THREADS) order[atomicAdd(&hist[key(b)], 1u)] = (int32_t)b;
 }
 
-// launch order of a cold solve (wave program): instances by the number of rows the warm start violates (the eval
-// hook's c / cl / cu / activity at u0), most first — a cheap predictor of the long instances (cfg2: 319 of the
-// 479 instances that take >= 25 iterations are in the top 958), so they start first.  One workgroup, a counting
-// sort (ties in any order); only the order changes, never an instance's arithmetic.
-constexpr int SOLVE_ORDER_MAX_B = 8192;   // cold-solve ordering for batches up to this size (one workgroup's LDS keys)
-__global__ __launch_bounds__(CL_ORDER_THREADS) void solve_order_kernel(const double* c, const double* cl, const double* cu,
-                                                                      const int8_t* act, int m, long long B, int32_t* order)
-{
-    constexpr int NK = 64;
-    __shared__ unsigned hist[NK];
-    __shared__ unsigned char keys[SOLVE_ORDER_MAX_B];
-    const int t = threadIdx.x;
-    auto key = [&](long long b) { return (int)keys[b]; };
-    if (t < NK) hist[t] = 0u;
-    // key = NK - 1 - (violated rows of the instance), computed once into LDS
-    for (long long b = t; b < B; b += CL_ORDER_THREADS) {
-        int v = 0;
-        for (int r = 0; r < m; ++r) {
-            const size_t o = (size_t)b * m + r;
-            const double cv = c[o];
-            v += (act[o] && (cv < cl[o] - 1e-6 || cv > cu[o] + 1e-6)) ? 1 : 0;
-        }
-        keys[b] = (unsigned char)(NK - 1 - (v > NK - 1 ? NK - 1 : v));
-    }
-    __syncthreads();
-    for (long long b = t; b < B; b += CL_ORDER_THREADS) atomicAdd(&hist[key(b)], 1u);
-    __syncthreads();
-    if (t == 0) {
-        unsigned acc = 0;
-        for (int k = 0; k < NK; ++k) {
-            const unsigned cnt = hist[k];
-            hist[k] = acc;
-            acc += cnt;
-        }
-    }
-    __syncthreads();
-    for (long long b = t; b < B; b += CL_ORDER_THREADS) order[atomicAdd(&hist[key(b)], 1u)] = (int32_t)b;
-}
-
 __global__ __launch_bounds__(256) void cl_update_kernel(CLP C)
 {
     const long long b = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -4283,9 +4280,6 @@ struct Handle {
     // rollout working set (evolving state, warm starts, per-step solve outputs)
     void* rstage = nullptr;
     size_t rstage_bytes = 0;
-    // cold-solve launch order: the eval hook's outputs at the warm start and the order (launch_solve_ordered)
-    void* ostage = nullptr;
-    size_t ostage_bytes = 0;
     hipStream_t own = nullptr;
     // launch timing: a ring of event pairs, so a re-record never targets an event still pending on the
     // stream (that serialises the host with the previous launch)
@@ -4788,42 +4782,6 @@ int alipmpc_create(const alipmpc_cfg* cfg, int device, void** handle)
     return ALIPMPC_OK;
 }
 
-// a solve launch of the wave program (cold solves of up to SOLVE_ORDER_MAX_B instances): the eval hook at the warm
-// start, solve_order_kernel, then the solve in that order — the instances predicted long start first.  Opt-in
-// (ALIPMPC_SOLVE_ORDER=1) until measured on the bench config; per-instance results are the same bits either way.
-static hipError_t launch_solve_ordered(Handle* h, KP P, hipStream_t st)
-{
-    const alipmpc_cfg& cf = h->cfg;
-    const char* oe = std::getenv("ALIPMPC_SOLVE_ORDER");
-    if (cf.variant == ALIPMPC_VARIANT_DD || cf.program == ALIPMPC_PROGRAM_LANE || P.order || P.B < 2 ||
-        P.B > SOLVE_ORDER_MAX_B || !P.u0 || !(oe && std::strcmp(oe, "1") == 0))
-        return launch(h, true, P, st);
-    const size_t Bz = (size_t)P.B, m = (size_t)h->m_max;
-    const size_t need = Bz * m * 8 * 3 + Bz * 4 + Bz * m + 256;
-    if (h->ostage_bytes < need) {
-        if (h->ostage) (void)hipFree(h->ostage);
-        h->ostage = nullptr;
-        h->ostage_bytes = 0;
-        if (hipError_t e = hipMalloc(&h->ostage, need)) return e;
-        h->ostage_bytes = need;
-    }
-    double* c = (double*)h->ostage;
-    double* cl = c + Bz * m;
-    double* cu = cl + Bz * m;
-    int32_t* ord = (int32_t*)(cu + Bz * m);
-    int8_t* act = (int8_t*)(ord + Bz);
-    KP E = make_kp(h, P.B, false);
-    E.x0 = P.x0; E.goal = P.goal; E.leg = P.leg; E.cir = P.cir; E.nc = P.nc; E.elp = P.elp; E.ne = P.ne;
-    E.u0 = P.u0; E.last_u = P.last_u;
-    E.c_out = c; E.cl_out = cl; E.cu_out = cu; E.active_out = act;
-    if (hipError_t e = launch(h, false, E, st)) return e;
-    hipLaunchKernelGGL(solve_order_kernel, dim3(1), dim3(CL_ORDER_THREADS), 0, st, (const double*)c, (const double*)cl,
-                       (const double*)cu, (const int8_t*)act, (int)m, (long long)P.B, ord);
-    if (hipError_t e = hipGetLastError()) return e;
-    P.order = ord;
-    return launch(h, true, P, st);
-}
-
 static int run_batch(Handle* h, bool solve, int64_t B, const double* x0, const double* goal, const int8_t* leg,
                      const double* cir, const int32_t* nc, const double* elp, const int32_t* ne, const double* u0,
                      const double* last_u, double* u_out, double* foot_out, double* x_pred, int32_t* status, int32_t* iters, double* f,
@@ -4854,7 +4812,7 @@ static int run_batch(Handle* h, bool solve, int64_t B, const double* x0, const d
         const int ei = h->evi;
         h->evi = (ei + 1) % Handle::NEV;
         HIPCHK(h, hipEventRecord(h->ev[ei][0], st));
-        HIPCHK(h, solve ? launch_solve_ordered(h, P, st) : launch(h, false, P, st));
+        HIPCHK(h, launch(h, solve, P, st));
         HIPCHK(h, hipEventRecord(h->ev[ei][1], st));
         h->evlast = ei;
         h->timed = true;
@@ -4936,7 +4894,7 @@ static int run_batch(Handle* h, bool solve, int64_t B, const double* x0, const d
     const int ei = h->evi;
     h->evi = (ei + 1) % Handle::NEV;
     HIPCHK(h, hipEventRecord(h->ev[ei][0], st));
-    HIPCHK(h, solve ? launch_solve_ordered(h, P, st) : launch(h, false, P, st));
+    HIPCHK(h, launch(h, solve, P, st));
     HIPCHK(h, hipEventRecord(h->ev[ei][1], st));
     h->evlast = ei;
     h->timed = true;
@@ -5236,6 +5194,14 @@ int alipmpc_closed_loop_batch(void* handle, int64_t B, int32_t S, int32_t f_cyc,
                 P.order = l.ord;
             }
             P.queue = h->dq + 2 * (h->qi.fetch_add(1u) % Handle::NQ);
+#ifdef ALIP_WSTAMP
+            {   // diagnostic record slots of this tick: (s f_cyc + i) B + instance
+                const long long base = ((long long)s * f_cyc + i) * B;
+                HIPCHK(h, hipMemcpyToSymbolAsync(HIP_SYMBOL(alip::g_wstamp_base), &base, sizeof(base), 0,
+                                                 hipMemcpyHostToDevice, st));
+                HIPCHK(h, hipStreamSynchronize(st));   // &base is a stack value
+            }
+#endif
             HIPCHK(h, launch(h, true, P, st));
             hipLaunchKernelGGL(cl_update_kernel, dim3(g1), dim3(256), 0, st, C);
             HIPCHK(h, hipGetLastError());
@@ -5385,6 +5351,29 @@ int alipmpc_dbg_stamps(unsigned long long* out, int reset)
 }
 #endif
 
+#ifdef ALIP_WSTAMP
+// diagnostic: copy the first `slots` per-instance records (8 values each) of the wave program and reset the base
+int alipmpc_dbg_wstamps(unsigned long long* out, long long slots)
+{
+    if (slots > alip::WSTAMP_CAP) slots = alip::WSTAMP_CAP;
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(alip::g_wstamp), sizeof(unsigned long long) * 8 * (size_t)slots) != hipSuccess)
+        return -1;
+    const long long z = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(alip::g_wstamp_base), &z, sizeof(z)) != hipSuccess) return -1;
+    return (int)slots;
+}
+#endif
+
+const char* alipmpc_build_id(void)
+{
+#ifdef ALIP_BUILD_ID
+    return ALIP_BUILD_ID;
+#else
+    return "unknown";
+#endif
+}
+
 double alipmpc_last_kernel_ms(void* handle)
 {
     Handle* h = (Handle*)handle;
@@ -5449,7 +5438,6 @@ void alipmpc_destroy(void* handle)
     if (h->dlk) hipFree(h->dlk);
     if (h->dlkf) hipFree(h->dlkf);
     if (h->stage) hipFree(h->stage);
-    if (h->ostage) hipFree(h->ostage);
     if (h->rstage) hipFree(h->rstage);
     for (auto& pr : h->ev)
         for (hipEvent_t e : pr)

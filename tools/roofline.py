@@ -9,6 +9,9 @@ The directory holds what tools/gpu_run.sh's `prof` step collects for ONE bench c
   prof_kt/kt_kernel_stats.csv      rocprofv3 --kernel-trace --stats of `bench.py --steps 10`
   pmc_*/pmc_counter_collection.csv rocprofv3 --pmc passes of `bench.py --steps 3 --warmup 1` (one pass each)
 
+Every record carries the alipmpc_build_id of the profiled library (bench.json config.build_id); bench.py attaches a
+record to its line only when that id equals the id of the library it is timing.
+
 Fields (per launch of the dominant solve kernel; the first dispatch of every pass is the warmup and skipped):
   kernel_ms          kernel-trace average duration (the bench's own HIP-event figure must agree)
   achieved / frac    algorithmic FP64 flops per launch (flops_per_iter x instance-iterations) / kernel_ms, / peak
@@ -61,7 +64,8 @@ def sweep(a):
     kern = "void alip::" + kname.replace(",", ", ")[:-1]
     c, meta = counters(a.dir, kern)
     ms, calls = kernel_ms(a.dir, kern)
-    out = {"kernel": kname, "B": a.batch, "bytes_per_instance": a.bytes, "kernel_ms_trace": ms, "trace_calls": calls}
+    out = {"kernel": kname, "B": a.batch, "bytes_per_instance": a.bytes, "kernel_ms_trace": ms, "trace_calls": calls,
+           "build_id": a.build_id, "profile_dir": a.dir}
     if ms:
         ach = a.batch * a.bytes / (ms * 1e-3) / 1e9
         out.update(achieved=ach, peak=8000.0, unit="GB/s", frac=ach / 8000.0)
@@ -89,8 +93,12 @@ def main():
     ap.add_argument("--sweep", default=None, help="Jacobian-sweep kernel name, e.g. 'sweep_kernel<5,true,32,2>'")
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--bytes", type=int, default=4272)
+    ap.add_argument("--build-id", default=None, help="--sweep: alipmpc_build_id of the profiled library "
+                    "(default: <dir>/build_id.txt)")
     a = ap.parse_args()
     if a.sweep:
+        if a.build_id is None and os.path.exists(os.path.join(a.dir, "build_id.txt")):
+            a.build_id = open(os.path.join(a.dir, "build_id.txt")).read().strip()
         return sweep(a)
     bench = json.load(open(os.path.join(a.dir, "bench.json")))
     rl = bench["roofline"]
@@ -101,7 +109,8 @@ def main():
     ms, calls = kernel_ms(a.dir, kern)
     its = rl["iters_per_launch"]
     out = {"kernel": kname, "B": bench["config"]["batch_per_gpu"], "N": bench["config"]["horizon"],
-           "dtype": bench["dtype"], "kernel_ms_trace": ms, "trace_calls": calls, "kernel_ms_bench": rl["kernel_ms"]}
+           "dtype": bench["dtype"], "build_id": bench["config"].get("build_id"), "profile_dir": a.dir,
+           "kernel_ms_trace": ms, "trace_calls": calls, "kernel_ms_bench": rl["kernel_ms"]}
     if ms:
         ach = rl["flops_per_iter"] * its / (ms * 1e-3) / 1e12
         out.update(achieved=ach, peak=rl["peak"], frac=ach / rl["peak"])
