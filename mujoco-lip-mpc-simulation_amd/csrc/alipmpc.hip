@@ -57,6 +57,7 @@ constexpr int MAX_ROWS = 128;        // padded constraint rows per instance (2 p
 constexpr int FILTER_CAP = 128;      // 2 filter entries per lane
 constexpr int REST_FAIL = 6;         // restoration events with violation > 1e-4 -> status 2
 
+
 typedef double d4 __attribute__((ext_vector_type(4)));
 
 // ------------------------------------------------------------------------------------------------
@@ -83,6 +84,11 @@ struct KP {
     uint32_t* queue;        // nullable: work-queue counters of a persistent solve launch (solve_kernel)
     const int32_t* order;   // nullable: launch order of the wave program (wave / queue slot k solves instance
                             // order[k]; the closed loop puts last tick's long instances first)
+    int ckpt_it;            // split launch, phase 1 (> 0): an instance still running at this iteration saves its
+                            // loop state to a record and stops (solve_kernel, one wave per instance)
+    int resume;             // split launch, phase 2: wave k resumes the instance of record k
+    double* ckpt;           // split launch: per-record loop state (ckpt_doubles(RPL) each)
+    uint32_t* cont;         // split launch: cont[0] = records written, cont[1 + k] = instance of record k
     // solve outputs
     double* u_out;
     double* foot_out;
@@ -104,6 +110,25 @@ struct KP {
 };
 
 constexpr int KP_DOUBLES = (int)((sizeof(KP) + 15) / 16 * 2);
+// split-launch record of one instance: per lane and row group the row state (slack, multipliers, inverse slack
+// distances, value, transcendentals, the 4 generator values), the filter entries (2 x 2) and the generator value
+// V[lane]; then 16 uniform values
+constexpr int CKPT_ROW = 12;
+__host__ __device__ constexpr int ckpt_doubles(int rpl) { return WAVE * (CKPT_ROW * rpl + 5) + 16; }
+#ifndef ALIP_SPLIT_IT
+#define ALIP_SPLIT_IT 16
+#endif
+constexpr int SPLIT_IT_DEFAULT = ALIP_SPLIT_IT;   // phase-1 iteration cap of the split launch (launch_solve)
+constexpr int ST_CKPT = 3;   // internal status of an instance whose loop state went to a split-launch record
+// record slots are doubles; an fp32 kernel's values are stored as their bit patterns (no conversion)
+__device__ __forceinline__ double ck_put(double v) { return v; }
+__device__ __forceinline__ double ck_put(float v) { return __longlong_as_double((long long)__float_as_uint(v)); }
+template <class R>
+__device__ __forceinline__ R ck_get(double d);
+template <>
+__device__ __forceinline__ double ck_get<double>(double d) { return d; }
+template <>
+__device__ __forceinline__ float ck_get<float>(double d) { return __uint_as_float((unsigned)__double_as_longlong(d)); }
 
 // R_FEN is the reference's f_en row (eval); in the solve layout (modi) it is the smooth half
 // vbx + s dth <= bvx_hi and R_FENM the other half vbx - s dth <= bvx_hi (see row_bounds)
@@ -1106,7 +1131,7 @@ __device__ __forceinline__ R obj_sum(const R (&v)[RPL], int mr4)
 }
 
 template <int N, int KSM, class R, bool Q>
-__device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int wv, long long b)
+__device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int wv, long long b, long long rec = -1)
 {
     // Q (persistent instance loop): opaque per-instance copies of the lane-/wave-derived inputs, so that
     // nothing computed from them is loop-invariant and no address or row table is hoisted out of the
@@ -1275,8 +1300,96 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
     bool theta_ok = false;
     const R gth = R(1e-5), gph = R(1e-8), sth = R(1.1), sph = R(2.3), eta = R(1e-8), gal = R(0.05);
 
+    int it0 = 0;
+    if (rec >= 0) {
+        // split launch, phase 2: the loop state at the top of iteration `it`, from the record phase 1 wrote (all
+        // of it: values the loop could recompute are stored too, so no recomputation can round differently).
+        const double* rc = P.ckpt + rec * ckpt_doubles(RPL);
+#pragma unroll
+        for (int q = 0; q < RPL; ++q) {
+            const double* rq = rc + WAVE * CKPT_ROW * q + lane;
+            sr[q] = ck_get<R>(rq[0]);
+            zl[q] = ck_get<R>(rq[WAVE]);
+            zu[q] = ck_get<R>(rq[2 * WAVE]);
+            idl[q] = ck_get<R>(rq[3 * WAVE]);
+            idu[q] = ck_get<R>(rq[4 * WAVE]);
+            cr[q] = ck_get<R>(rq[5 * WAVE]);
+            ra0[q] = ck_get<R>(rq[6 * WAVE]);
+            ra1[q] = ck_get<R>(rq[7 * WAVE]);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) rv[q][i] = ck_get<R>(rq[(8 + i) * WAVE]);
+        }
+        const double* rf = rc + WAVE * CKPT_ROW * RPL + lane;
+        fth0 = ck_get<R>(rf[0]);
+        fph0 = ck_get<R>(rf[WAVE]);
+        fth1 = ck_get<R>(rf[2 * WAVE]);
+        fph1 = ck_get<R>(rf[3 * WAVE]);
+        vme = lane < NG ? ck_get<R>(rf[4 * WAVE]) : R(0.0);
+        const double* sc = rc + WAVE * (CKPT_ROW * RPL + 5);
+        mu = uni(ck_get<R>(sc[0]));
+        f_cur = uni(ck_get<R>(sc[1]));
+        lsum_cur = uni(ck_get<R>(sc[2]));
+        theta_c = uni(ck_get<R>(sc[3]));
+        dw_last = uni(ck_get<R>(sc[4]));
+        nf = rfl((int)sc[5]);
+        it0 = rfl((int)sc[6]);
+        n_rest = rfl((int)sc[7]);
+        fail_it = rfl((int)sc[8]);
+        it_end = rfl((int)sc[9]);
+        theta_ok = rfl((int)sc[10]) != 0;
+        if (lane < NG) w.V[lane] = vme;
+        wave_sync();
+#ifndef ALIP_NO_SETPRIO
+        if (it0 >= 20)
+            __builtin_amdgcn_s_setprio(3);
+        else if (it0 >= 14)
+            __builtin_amdgcn_s_setprio(2);
+        else if (it0 >= 8)
+            __builtin_amdgcn_s_setprio(1);
+#endif
+    }
+    const int ckpt_it = rfl(P.ckpt_it);
+
     STAMP_DECL
-    for (it = 0; it <= max_iter; ++it) {
+    for (it = it0; it <= max_iter; ++it) {
+        // split launch, phase 1: an instance still running at iteration ckpt_it writes its loop state to the next
+        // record and stops; phase 2 resumes it on a wave of its own (the long instances no longer share SIMDs)
+        if (ckpt_it > 0 && it == ckpt_it) {
+            int k = 0;
+            if (lane == 0) k = (int)atomicAdd(P.cont, 1u);
+            k = rfl(k);
+            double* rc = P.ckpt + (long long)k * ckpt_doubles(RPL);
+#pragma unroll
+            for (int q = 0; q < RPL; ++q) {
+                double* rq = rc + WAVE * CKPT_ROW * q + lane;
+                rq[0] = ck_put(sr[q]);
+                rq[WAVE] = ck_put(zl[q]);
+                rq[2 * WAVE] = ck_put(zu[q]);
+                rq[3 * WAVE] = ck_put(idl[q]);
+                rq[4 * WAVE] = ck_put(idu[q]);
+                rq[5 * WAVE] = ck_put(cr[q]);
+                rq[6 * WAVE] = ck_put(ra0[q]);
+                rq[7 * WAVE] = ck_put(ra1[q]);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) rq[(8 + i) * WAVE] = ck_put(rv[q][i]);
+            }
+            double* rf = rc + WAVE * CKPT_ROW * RPL + lane;
+            rf[0] = ck_put(fth0);
+            rf[WAVE] = ck_put(fph0);
+            rf[2 * WAVE] = ck_put(fth1);
+            rf[3 * WAVE] = ck_put(fph1);
+            rf[4 * WAVE] = ck_put(vme);
+            const double sv[11] = {ck_put(mu), ck_put(f_cur), ck_put(lsum_cur), ck_put(theta_c), ck_put(dw_last),
+                                   (double)nf, (double)it, (double)n_rest, (double)fail_it, (double)it_end,
+                                   theta_ok ? 1.0 : 0.0};
+            double v = 0.0;
+#pragma unroll
+            for (int i = 0; i < 11; ++i) v = lane == i ? sv[i] : v;
+            if (lane < 11) rc[WAVE * (CKPT_ROW * RPL + 5) + lane] = v;
+            if (lane == 0) P.cont[1 + k] = (uint32_t)b;
+            status = ST_CKPT;
+            break;
+        }
         // A batch finishes with its slowest instance, and the 4 waves sharing a SIMD compete for issue: waves
         // that have run long get priority, so the critical (high-iteration) instances run closer to their
         // lone-wave latency while the short ones, which have slack, yield.
@@ -1802,6 +1915,10 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
     }
     STAMP(8);
     STAMP_FLUSH;
+    if (status == ST_CKPT) {   // phase 2 of the split launch finishes this instance
+        WSTAMP_WRITE(b, it, n_rest);
+        return;
+    }
     if (fail_it >= 0) {   // the last iterate, as IPOPT returns it with Error_In_Step_Computation
         status = -3;
         it = fail_it;
@@ -1829,7 +1946,7 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
         else if (viol > R(1e-4))
             status = 2;
     }
-    WSTAMP_WRITE(b, it, n_rest);
+    WSTAMP_WRITE(rec >= 0 ? P.B + rec : b, it, n_rest);   // (diagnostic build: phase-2 records after the batch's)
     // canonical u: u_k = x_{k+1} (W u_k = p_k since W B = I) — the reference's "desired next state"
     if (lane < 5 * N) P.u_out[(size_t)b * 5 * N + lane] = w.V[gx(lane / 5 + 1, lane % 5)];
     if (P.foot_out && lane < 3) P.foot_out[3 * b + lane] = w.V[gp(0, lane)];
@@ -1911,15 +2028,29 @@ __global__ __launch_bounds__(256, (solve_waves<KSM, R>())) void solve_kernel(KP 
     // the per-instance arithmetic does not depend on the slot, only when and where the instance runs
     if constexpr (ONE) {
         const long long k = (long long)blockIdx.x * WAVES_PER_BLOCK + wv;
-        if (k < Pv.B) {
-            const long long b = Pv.order ? (long long)__builtin_amdgcn_readfirstlane(Pv.order[k]) : k;
-            if (!Pv.active || Pv.active[b]) solve_one<N, KSM, R, false>(P, G, E, wsb, wv, b);
+        long long b = -1, rec = -1;   // one inlined solve_one for both forms (the code is large)
+        if (Pv.resume) {   // split launch, phase 2: wave k finishes the instance of record k
+            const long long cnt = (long long)__builtin_amdgcn_readfirstlane(Pv.cont[0]);
+            if (k < cnt) {
+                b = (long long)__builtin_amdgcn_readfirstlane(Pv.cont[1 + k]);
+                rec = k;
+            }
+        } else if (k < Pv.B) {
+            b = Pv.order ? (long long)__builtin_amdgcn_readfirstlane(Pv.order[k]) : k;
+            if (Pv.active && !Pv.active[b]) b = -1;
         }
+        b = __builtin_amdgcn_readfirstlane((int)b);
+        rec = __builtin_amdgcn_readfirstlane((int)rec);
+        if (b >= 0) solve_one<N, KSM, R, false>(P, G, E, wsb, wv, b, rec);
     } else {
         uint32_t* const q = Pv.queue;
         for (long long k = next_instance(q); k < Pv.B; k = next_instance(q)) {
             const long long b = Pv.order ? (long long)__builtin_amdgcn_readfirstlane(Pv.order[k]) : k;
-            if (!Pv.active || Pv.active[b]) solve_one<N, KSM, R, true>(P, G, E, wsb, wv, b);   // rollout: skip finished
+            // (no split records in this form; the record index is opaque so that both forms compile the same
+            // solve_one — fp32 contraction / packing decisions otherwise differ between them)
+            long long rec = -1;
+            asm volatile("" : "+s"(rec));
+            if (!Pv.active || Pv.active[b]) solve_one<N, KSM, R, true>(P, G, E, wsb, wv, b, rec);   // rollout: skip finished
         }
         queue_exit(q);
     }
@@ -4281,6 +4412,15 @@ struct Handle {
     void* rstage = nullptr;
     size_t rstage_bytes = 0;
     hipStream_t own = nullptr;
+    // split launch of the wave program (ALIPMPC_SPLIT_IT): the phase-1 iteration cap (0 = off) and, per stream, the
+    // record buffer (launches on one stream run in order, so they may share it; other streams get their own)
+    int split_it = 0;
+    struct SplitBuf {
+        void* p = nullptr;
+        size_t bytes = 0;
+    };
+    std::map<hipStream_t, SplitBuf> split;
+    std::mutex split_mtx;
     // launch timing: a ring of event pairs, so a re-record never targets an event still pending on the
     // stream (that serialises the host with the previous launch)
     static constexpr int NEV = 16;
@@ -4766,6 +4906,11 @@ int alipmpc_create(const alipmpc_cfg* cfg, int device, void** handle)
         if (h->cfg.variant != ALIPMPC_VARIANT_DD && h->cfg.N == 3 && h->cfg.ne_max == 0 && h->cfg.nc_max <= 6 &&
             !(ek && std::strcmp(ek, "group") == 0))
             h->sweep_nc = h->cfg.nc_max;
+        {   // split launch of one-wave-per-instance batches (ALIPMPC_SPLIT_IT=0 turns it off)
+            const char* se = std::getenv("ALIPMPC_SPLIT_IT");
+            h->split_it = se ? std::atoi(se) : SPLIT_IT_DEFAULT;
+            if (h->split_it < 0 || h->split_it >= h->cfg.max_iter) h->split_it = 0;
+        }
         if (h->cfg.program == ALIPMPC_PROGRAM_LANE) {
             h->lane_nct = lane_slots_for(h->cfg);
             if (h->lane_nct < 0) {
@@ -4780,6 +4925,53 @@ int alipmpc_create(const alipmpc_cfg* cfg, int device, void** handle)
     }
     *handle = h;
     return ALIPMPC_OK;
+}
+
+// A wave-program solve whose batch fits the resident slots (one wave per instance) runs as a SPLIT launch: phase 1
+// solves every instance for up to split_it iterations; an instance still running then writes its loop state to a
+// record and stops; phase 2 resumes those instances, one wave each.  The long instances (cfg2: 12 % run to the
+// 30-iteration cap) otherwise finish at the pace of the busiest SIMDs, which hold two or three of them
+// among their four waves; in phase 2 they are few enough for a SIMD each.  Every instance executes the same
+// arithmetic either way (the record holds its exact loop state): same bits (test_split_launch_bit_identical).
+static hipError_t launch_solve(Handle* h, const KP& P, hipStream_t st)
+{
+    const alipmpc_cfg& cf = h->cfg;
+    if (cf.variant == ALIPMPC_VARIANT_DD || h->lane_nct >= 0 || h->split_it <= 0 || P.B < 2 || P.active || P.order)
+        return launch(h, true, P, st);
+    unsigned res = 0;
+    if (hipError_t e = launch(h, true, P, st, &res)) return e;
+    if ((long long)res * WAVES_PER_BLOCK < P.B) return launch(h, true, P, st);   // the work-queue form
+    const size_t rpl = (size_t)((h->mo4 + WAVE - 1) / WAVE);
+    const size_t rec_bytes = ((size_t)P.B * ckpt_doubles((int)rpl) * sizeof(double) + 255) & ~(size_t)255;
+    const size_t need = rec_bytes + ((size_t)P.B + 1) * sizeof(uint32_t);
+    void* buf = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(h->split_mtx);
+        Handle::SplitBuf& sb = h->split[st];
+        if (sb.bytes < need) {
+            hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+            if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone)
+                return launch(h, true, P, st);   // no allocation inside a capture: the one-phase form
+            if (sb.p) (void)hipFree(sb.p);
+            sb.p = nullptr;
+            sb.bytes = 0;
+            if (hipError_t e = hipMalloc(&sb.p, need)) return e;
+            sb.bytes = need;
+        }
+        buf = sb.p;
+    }
+    uint32_t* cont = reinterpret_cast<uint32_t*>((char*)buf + rec_bytes);
+    if (hipError_t e = hipMemsetAsync(cont, 0, sizeof(uint32_t), st)) return e;
+    KP P1 = P;
+    P1.ckpt_it = h->split_it;
+    P1.ckpt = (double*)buf;
+    P1.cont = cont;
+    if (hipError_t e = launch(h, true, P1, st)) return e;
+    KP P2 = P;
+    P2.resume = 1;
+    P2.ckpt = (double*)buf;
+    P2.cont = cont;
+    return launch(h, true, P2, st);
 }
 
 static int run_batch(Handle* h, bool solve, int64_t B, const double* x0, const double* goal, const int8_t* leg,
@@ -4812,7 +5004,7 @@ static int run_batch(Handle* h, bool solve, int64_t B, const double* x0, const d
         const int ei = h->evi;
         h->evi = (ei + 1) % Handle::NEV;
         HIPCHK(h, hipEventRecord(h->ev[ei][0], st));
-        HIPCHK(h, launch(h, solve, P, st));
+        HIPCHK(h, solve ? launch_solve(h, P, st) : launch(h, false, P, st));
         HIPCHK(h, hipEventRecord(h->ev[ei][1], st));
         h->evlast = ei;
         h->timed = true;
@@ -4894,7 +5086,7 @@ static int run_batch(Handle* h, bool solve, int64_t B, const double* x0, const d
     const int ei = h->evi;
     h->evi = (ei + 1) % Handle::NEV;
     HIPCHK(h, hipEventRecord(h->ev[ei][0], st));
-    HIPCHK(h, launch(h, solve, P, st));
+    HIPCHK(h, solve ? launch_solve(h, P, st) : launch(h, false, P, st));
     HIPCHK(h, hipEventRecord(h->ev[ei][1], st));
     h->evlast = ei;
     h->timed = true;
@@ -5169,9 +5361,11 @@ int alipmpc_closed_loop_batch(void* handle, int64_t B, int32_t S, int32_t f_cyc,
     P.goal = d_goal; P.cir = d_cir; P.nc = d_nc; P.elp = d_elp; P.ne = d_ne;
     P.x0 = l.xs; P.leg = l.sleg; P.u0 = l.u0; P.active = l.act;
     P.u_out = l.u; P.foot_out = l.foot; P.x_pred = l.xp; P.status = l.st; P.iters = l.it;
-    // launch ordering (wave program only; ALIPMPC_CL_ORDER=0 turns it off for A/B and the bit-identity test)
+    // longest-first launch order of each tick (wave program; opt-in, ALIPMPC_CL_ORDER=1): it puts at most one long
+    // instance on a SIMD, but a tick's time is set by its single slowest instance, a warm-started one whose line
+    // search halves ~20 times per iteration (tools/cl_wstamps.py, profiles/r3/wst): 52.13 vs 52.00 ms per loop
     const char* oe = std::getenv("ALIPMPC_CL_ORDER");
-    const bool order_ok = cf.program != ALIPMPC_PROGRAM_LANE && !(oe && std::strcmp(oe, "0") == 0);
+    const bool order_ok = cf.program != ALIPMPC_PROGRAM_LANE && oe && std::strcmp(oe, "1") == 0;
     const int ei = h->evi;
     h->evi = (ei + 1) % Handle::NEV;
     HIPCHK(h, hipEventRecord(h->ev[ei][0], st));
@@ -5361,6 +5555,10 @@ int alipmpc_dbg_wstamps(unsigned long long* out, long long slots)
         return -1;
     const long long z = 0;
     if (hipMemcpyToSymbol(HIP_SYMBOL(alip::g_wstamp_base), &z, sizeof(z)) != hipSuccess) return -1;
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(alip::g_wstamp)) != hipSuccess ||
+        hipMemset(p, 0, sizeof(unsigned long long) * 8 * (size_t)alip::WSTAMP_CAP) != hipSuccess)
+        return -1;
     return (int)slots;
 }
 #endif
@@ -5439,6 +5637,8 @@ void alipmpc_destroy(void* handle)
     if (h->dlkf) hipFree(h->dlkf);
     if (h->stage) hipFree(h->stage);
     if (h->rstage) hipFree(h->rstage);
+    for (auto& kv : h->split)
+        if (kv.second.p) hipFree(kv.second.p);
     for (auto& pr : h->ev)
         for (hipEvent_t e : pr)
             if (e) hipEventDestroy(e);

@@ -94,21 +94,46 @@ def run(args):
     cfg = alipmpc.default_cfg(alipmpc.VARIANT_MODI, N, nc_max=5, ne_max=0)
     s = alipmpc.Solver(cfg, device=0)
     buf = np.zeros((48 * 4096, 8), np.uint64)
+    os.makedirs(args.out, exist_ok=True)
 
     def grab(slots):
         rc = L.alipmpc_dbg_wstamps(buf.ctypes.data_as(ctypes.c_void_p), slots)
         assert rc == slots, rc
         return buf[:slots].copy()
 
-    res = {"build_id": alipmpc.build_id(), "cold": [], "closed_loop": {}}
+    res = {"build_id": alipmpc.build_id(), "cold": [], "closed_loop": {}, "split": {}}
     for _ in range(3):
         out = s.solve(bt["x0"], bt["goal"], bt["leg"], bt["cir"], bt["nc"], u0=bt["u0"])
         rec = grab(B)
         res["cold"].append(summarize(rec, tag=f"cold {s.last_kernel_ms():.3f} ms"))
-        buf[:B] = 0
+        buf[:2 * B] = 0
     print(json.dumps(res["cold"][-1]))
+    np.save(os.path.join(args.out, "cold_records.npy"), rec) if os.path.isdir(args.out) else None
+    # split launches: phase-1 records in slots [0, B), phase-2 records in [B, 2B)
+    for cut in args.cuts:
+        os.environ["ALIPMPC_SPLIT_IT"] = str(cut)
+        ss = alipmpc.Solver(cfg, device=0)
+        for _ in range(3):
+            buf[:2 * B] = 0
+            ss.solve(bt["x0"], bt["goal"], bt["leg"], bt["cir"], bt["nc"], u0=bt["u0"])
+            rec = grab(2 * B)
+        ms = ss.last_kernel_ms()
+        p1, p2 = rec[:B], rec[B:]
+        n2 = int((p2[:, 1] > 0).sum())
+        base = int(p1[p1[:, 1] > 0, 0].min())
+        e1 = (int(p1[p1[:, 1] > 0, 1].max()) - base) / 100.0
+        s2 = (int(p2[p2[:, 1] > 0, 0].min()) - base) / 100.0 if n2 else None
+        e2 = (int(p2[p2[:, 1] > 0, 1].max()) - base) / 100.0 if n2 else None
+        r = {"cut": cut, "launch_ms": ms, "phase1_end_us": e1, "phase2_start_us": s2, "phase2_end_us": e2,
+             "phase2_instances": n2, "phase1": summarize(p1, tag=f"split {cut} phase 1"),
+             "phase2": summarize(p2, tag=f"split {cut} phase 2") if n2 else None}
+        res["split"][str(cut)] = r
+        print(json.dumps({k: v for k, v in r.items() if k not in ("phase1", "phase2")}))
+        print(json.dumps(r["phase1"]))
+        print(json.dumps(r["phase2"]))
+    os.environ["ALIPMPC_SPLIT_IT"] = "0"
     foot0 = out["foot"][:, 0:2].copy()
-    for order in ("0", "1"):
+    for order in (() if args.no_closed_loop else ("0", "1")):
         os.environ["ALIPMPC_CL_ORDER"] = order
         sc = alipmpc.Solver(cfg, device=0)
         F = 40
@@ -136,5 +161,7 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("what", choices=["build", "run"])
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "wst"))
+    ap.add_argument("--cuts", type=int, nargs="*", default=[16])
+    ap.add_argument("--no-closed-loop", action="store_true")
     a = ap.parse_args()
     build() if a.what == "build" else run(a)
