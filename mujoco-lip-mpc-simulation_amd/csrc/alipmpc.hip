@@ -119,6 +119,9 @@ __host__ __device__ constexpr int ckpt_doubles(int rpl) { return WAVE * (CKPT_RO
 #define ALIP_SPLIT_IT 16
 #endif
 constexpr int SPLIT_IT_DEFAULT = ALIP_SPLIT_IT;   // phase-1 iteration cap of the split launch (launch_solve)
+#ifndef ALIP_GJ_REGS
+#define ALIP_GJ_REGS 1
+#endif
 constexpr int ST_CKPT = 3;   // internal status of an instance whose loop state went to a split-launch record
 // record slots are doubles; an fp32 kernel's values are stored as their bit patterns (no conversion)
 __device__ __forceinline__ double ck_put(double v) { return v; }
@@ -811,6 +814,28 @@ __device__ __forceinline__ bool gj_lds(R* M, int lane)
     return true;
 }
 
+// The same Gauss-Jordan elimination with the rows in registers: lane i (< n) holds row i of [K + dw I | rhs] in
+// a[0..n]; step p reads the pivot row's entries j > p by readlane (uniform), scales them by 1 / pivot and updates
+// every other row — gj_lds's arithmetic element for element, without an LDS round trip per step (the steps are a
+// readlane -> rcp -> fma chain).  On success lane i holds x_i in a[n].
+template <int n, class R>
+__device__ __forceinline__ bool gj_regs(R (&a)[n + 1], int lane)
+{
+#pragma unroll
+    for (int p = 0; p < n; ++p) {
+        const R d = bcast(a[p], p);
+        if (!(d > R(0))) return false;   // wave-uniform
+        const R inv = rcp_nr(d);
+        const R f = a[p];
+#pragma unroll
+        for (int j = p + 1; j <= n; ++j) {
+            const R pj = bcast(a[j], p) * inv;
+            a[j] = lane == p ? pj : fma(-f, pj, a[j]);
+        }
+    }
+    return true;
+}
+
 // working copy for gj_lds: M[i][j] = K[i][j] + dw [i == j] (j <= n; column n = rhs), same element
 // ownership as gj_lds (the padding element M[n][n] = 0)
 template <int n, int LDK, int LD, class R>
@@ -1149,6 +1174,7 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
     constexpr bool JC = KSM * NT <= 16;   // keep the J tile in registers between the two J-layout passes
     constexpr bool GJ = n <= 9;           // KKT solve: LDS Gauss-Jordan (small n) or register Cholesky
     constexpr int GJLD = n + 1;           // row stride of the Gauss-Jordan working copy (in the S buffer)
+    constexpr bool GJ_REGS = ALIP_GJ_REGS != 0;   // Gauss-Jordan on register rows (gj_regs) instead of LDS
     static_assert((n + 1) * (n + 1) <= 64 * (N + 1), "GJ working copy fits the S-block buffer");
     static_assert(NG <= WAVE, "one generator row per lane");
     int lane = lane_id();
@@ -1618,7 +1644,30 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
             R rhs_l = R(0.0);
 #pragma unroll
             for (int T = 0; T < NT; ++T) rhs_l = (lane < n && (lane >> 4) == T) ? rhsc[T] : rhs_l;
-            if constexpr (GJ) {
+            if constexpr (GJ && GJ_REGS) {
+                // [K | rhs] rows in registers (K stays in w.K for inertia-correction retries)
+                R a[n + 1];
+                auto fill = [&](R dw) {
+#pragma unroll
+                    for (int j = 0; j < n; ++j) a[j] = (lane < n ? w.K[lane * KLD + j] : R(0.0)) + (lane == j ? dw : R(0.0));
+                    a[n] = rhs_l + R(0.0);
+                };
+                fill(R(0));
+                if (!gj_regs<n>(a, lane)) {
+                    R dw = dw_last == R(0.0) ? R(1e-4) : fmax(R(1e-20), dw_last / R(3.0));
+                    for (;;) {
+                        fill(dw);
+                        if (gj_regs<n>(a, lane)) break;
+                        dw *= dw_last == R(0.0) ? R(100.0) : R(8.0);
+                        if (dw > R(sizeof(R) == 8 ? 1e40 : 1e30)) {
+                            fact_ok = false;
+                            break;
+                        }
+                    }
+                    dw_last = uni(dw);
+                }
+                xv = lane < n ? a[n] : R(0.0);
+            } else if constexpr (GJ) {
                 // [K | rhs] stays in w.K (the original, for inertia-correction retries); the elimination runs on
                 // a copy in the S-block buffer, which is dead once K is built and is re-zeroed after dV below
                 if (lane < n) w.K[lane * KLD + n] = rhs_l;
@@ -1694,7 +1743,7 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
             R v = R(0.0);
 #pragma unroll
             for (int j = 0; j < n; ++j)
-                v += G[(lane < NG ? lane : 0) * NCP + j] * (GJ ? w.S[j * GJLD + n] : bcast(xv, j));
+                v += G[(lane < NG ? lane : 0) * NCP + j] * (GJ && !GJ_REGS ? w.S[j * GJLD + n] : bcast(xv, j));
             // a factorisation the regularisation could not rescue: zero step (the iterate stays), and the
             // solve ends at the next iteration's test with status -3 (no extra loop exit here: an exit
             // edge in mid-iteration lengthens live ranges and costs spills)
@@ -1702,7 +1751,7 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
             if (lane < NG) w.dV[lane] = dvme;
         }
         wave_sync();
-        if constexpr (GJ) gj_zero<n, GJLD>(w.S, lane);   // hess_blocks writes only the nonzero pattern of S
+        if constexpr (GJ && !GJ_REGS) gj_zero<n, GJLD>(w.S, lane);   // hess_blocks writes only the nonzero pattern of S
         if (!fact_ok && fail_it < 0) {
             fail_it = it;
             it_end = it + 1;

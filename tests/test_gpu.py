@@ -636,26 +636,36 @@ def test_work_queue_batch_independence(gpu_lib, variant, N, n_cir, n_elp, prec):
         assert np.array_equal(np.nan_to_num(r_big[k], nan=7.0), np.nan_to_num(r_small[k], nan=7.0)), k
 
 
-BENCH_KERNELS = [  # the kernel instance each BASELINE bench number comes from, at B > resident slots
-    ("cfg5", 0, 3, 5, 0, 1), ("cfg3", 0, 5, 5, 5, 0), ("cfg4", 0, 3, 5, 0, 0)]
+BENCH_KERNELS = [  # the program each BASELINE bench number comes from (bench.CONFIGS), at B > resident slots; the
+    # wave-program rows of the N = 3 shapes are kept as separate cases
+    ("cfg5", 0, 3, 5, 0, 1, "lane"), ("cfg4", 0, 3, 5, 0, 0, "lane"), ("cfg3", 0, 5, 5, 5, 0, "wave"),
+    ("cfg5", 0, 3, 5, 0, 1, "wave"), ("cfg4", 0, 3, 5, 0, 0, "wave")]
 
 
-@pytest.mark.parametrize("name,variant,N,n_cir,n_elp,prec", BENCH_KERNELS)
-def test_bench_kernels_beyond_resident_slots_vs_oracle(gpu_lib, coracle, name, variant, N, n_cir, n_elp, prec):
-    """The exact solve program and scene generator bench.py measures for cfg3 / cfg4 / cfg5, at a batch
-    above the resident slots (the persistent work queue cycles every wave through several instances),
-    against the fp64 C oracle on a fixed random subset of 2,048 instances.  Bars: fp64 as
-    test_solve_variants_vs_oracle (cfg3) / test_solve_cfg2_batch_vs_oracle (cfg4); fp32 as
-    test_fp32_solve_vs_oracle (foothold within 1e-3 where both converge)."""
-    from alipmpc import scenes
-    kw = dict(nc_max=n_cir, ne_max=n_elp)
+@pytest.mark.parametrize("name,variant,N,n_cir,n_elp,prec,program", BENCH_KERNELS)
+def test_bench_kernels_beyond_resident_slots_vs_oracle(gpu_lib, coracle, name, variant, N, n_cir, n_elp, prec,
+                                                       program):
+    """The solve program and scene generator bench.py measures for cfg3 / cfg4 / cfg5 (bench.CONFIGS: the lane
+    program for cfg4 / cfg5, the wave program for cfg3; bench.global_inputs), at a batch above the program's resident
+    slots (the persistent work queue cycles every wave / lane through several instances), against the fp64 C oracle
+    on a fixed random subset of 2,048 instances.  Bars: fp64 as test_solve_variants_vs_oracle (cfg3) /
+    test_solve_cfg2_batch_vs_oracle (cfg4); fp32 as test_fp32_solve_vs_oracle (foothold within 1e-3 where both
+    converge)."""
+    import bench
+    if program == "lane":
+        assert bench.CONFIGS[name]["program"] == "lane"
+    kw = dict(nc_max=n_cir, ne_max=n_elp,
+              program=gpu_lib.PROGRAM_LANE if program == "lane" else gpu_lib.PROGRAM_WAVE)
     if prec:
         kw["precision"] = gpu_lib.PREC_FP32
     s = gpu_lib.Solver(gpu_lib.default_cfg(variant, N, **kw))
+    assert s.solve_program().startswith("lane_kernel" if program == "lane" else "solve_kernel")
     slots = s.solve_slots()
-    B = 2 * slots + 123
-    bt = scenes.make_batch_vec(B, seed=500 + N + 10 * prec, n_cir=n_cir, n_elp=n_elp, N=N,
-                               fields=4096 if name == "cfg3" else None)
+    B = slots + slots // 8 + 123
+    block = 65536 if name == "cfg3" else bench.BLOCK[name]
+    bt = bench.global_inputs(name, 0, B, block, 5, n_cir, n_elp, N)
+    bt.setdefault("elp", None)
+    bt.setdefault("ne", None)
     o = s.solve(bt["x0"], bt["goal"], bt["leg"], bt["cir"], bt["nc"], bt["elp"], bt["ne"], u0=bt["u0"])
     idx = np.sort(np.random.default_rng(9).choice(B, 2048, replace=False))
     sub = {k: (None if v is None else v[idx]) for k, v in bt.items()}

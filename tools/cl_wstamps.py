@@ -143,6 +143,10 @@ def run(args):
                                steps=1, f_cyc=F)
             ms = sc.last_kernel_ms()
             rec = grab(F * B).reshape(F, B, 8)
+        # per tick and instance: duration (us), iterations, line-search trials (which episodes set each tick's time)
+        dur = (rec[:, :, 1].astype(np.int64) - rec[:, :, 0].astype(np.int64)) / 100.0
+        np.savez_compressed(os.path.join(args.out, f"cl_order{order}_per_instance.npz"), dur=dur,
+                            iters=rec[:, :, 5].astype(np.int32), trials=rec[:, :, 6].astype(np.int32))
         ticks = []
         for i in range(F):
             act = o["status"][:, 0, i] != alipmpc.ROLLOUT_DONE
