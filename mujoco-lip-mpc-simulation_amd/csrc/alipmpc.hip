@@ -122,6 +122,9 @@ constexpr int SPLIT_IT_DEFAULT = ALIP_SPLIT_IT;   // phase-1 iteration cap of th
 #ifndef ALIP_GJ_REGS
 #define ALIP_GJ_REGS 1
 #endif
+#ifndef ALIP_GJ_MAX_N   // largest KKT size solved by Gauss-Jordan (register rows); larger n: register Cholesky
+#define ALIP_GJ_MAX_N 15  // (cfg3, n = 15: 16.14 -> 15.51 ms per launch against the Cholesky)
+#endif
 constexpr int ST_CKPT = 3;   // internal status of an instance whose loop state went to a split-launch record
 // record slots are doubles; an fp32 kernel's values are stored as their bit patterns (no conversion)
 __device__ __forceinline__ double ck_put(double v) { return v; }
@@ -1172,7 +1175,7 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
     constexpr int KLD = D::KLD;
     constexpr int RPL = (4 * KSM + WAVE - 1) / WAVE;
     constexpr bool JC = KSM * NT <= 16;   // keep the J tile in registers between the two J-layout passes
-    constexpr bool GJ = n <= 9;           // KKT solve: LDS Gauss-Jordan (small n) or register Cholesky
+    constexpr bool GJ = n <= ALIP_GJ_MAX_N;   // KKT solve: Gauss-Jordan (small n) or register Cholesky
     constexpr int GJLD = n + 1;           // row stride of the Gauss-Jordan working copy (in the S buffer)
     constexpr bool GJ_REGS = ALIP_GJ_REGS != 0;   // Gauss-Jordan on register rows (gj_regs) instead of LDS
     static_assert((n + 1) * (n + 1) <= 64 * (N + 1), "GJ working copy fits the S-block buffer");
