@@ -204,6 +204,10 @@ def main():
     except (AttributeError, RuntimeError):
         slots = None
     kname = solver.solve_program()
+    try:
+        launches, team = solver.solve_launches(B)
+    except (AttributeError, RuntimeError):
+        launches, team = 1, 1
     m = solve_rows(N, solver.rps, variant == alipmpc.VARIANT_MODI)
     fpi = flops_per_iter(n, m, N, n_cir + n_elp)
     # the lane program's KKT system is fp64 in both precisions; its bound is vector issue (FP64 VALU peak =
@@ -261,8 +265,13 @@ def main():
                 "resident_slots": slots,
                 "program": program,
                 "launch": ("persistent work queue, one instance per lane" if program == "lane" else
+                           ("split launch: phase 1 one wavefront per instance up to the iteration cut, phase 2 "
+                            "resumes the unfinished instances" + (" (trial-cut ones on 4-wave teams)" if team > 1 else
+                                                                  " one wavefront each"))
+                           if launches == 2 else
                            "one wavefront per instance (B <= resident slots, no queue)" if slots and B <= slots else
                            "persistent work queue, one instance per wavefront"),
+                "launches_per_solve": launches,
                 "build_id": bid,
             },
             "roofline": {

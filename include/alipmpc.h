@@ -266,12 +266,21 @@ int alipmpc_trace_batch(void* handle, int64_t B, const double* x0, const double*
                         void* hip_stream);
 
 /* Instances this handle's solve kernel holds resident on its device at once (solve_kernel: resident
- * workgroups x 4 waves, one instance per wave; lane_kernel: resident waves x instances per wave).  Every LIP solve / rollout launch is a persistent grid of at most the
- * resident workgroups whose waves pull instances from a per-launch work queue (a wave that finishes a
- * short solve takes the next instance), so one program solves every batch size and an instance's result
- * does not depend on B (a batch solved whole or in chunks is bit-identical).  0 for the DD variant
- * (always one wave per instance).  No reference counterpart (scheduling of the batched replacement). */
+ * workgroups x 4 waves, one instance per wave; lane_kernel: resident waves x instances per wave).  A wave-program
+ * batch that fits these slots launches one wave per instance (as a split launch, see alipmpc_solve_launches); a
+ * larger one — and every lane-program batch — runs as a persistent grid of the resident workgroups whose waves
+ * (lanes) pull instances from a per-launch work queue.  Every form runs the same per-instance arithmetic, so an
+ * instance's result does not depend on B (a batch solved whole or in chunks is bit-identical).  0 for the DD
+ * variant (always one wave per instance).  No reference counterpart (scheduling of the batched replacement). */
 int alipmpc_solve_slots(void* handle, int64_t* slots);
+
+/* Kernel launches one alipmpc_solve_batch of B instances runs on this handle: 2 for a split launch (wave program,
+ * 2 <= B <= alipmpc_solve_slots, ALIPMPC_SPLIT_IT > 0: phase 1 up to that many iterations, phase 2 resumes the
+ * unfinished instances from their exact loop-state records), 1 otherwise; *team = 4 when phase 1 also cuts instances
+ * by their line-search trial count (ALIPMPC_SPLIT_TR > 0, fp64 only) into team records that phase 2 runs on 4 waves
+ * each, else 1.
+ * Profiling tools use it to turn per-dispatch figures into per-solve ones.  No reference counterpart. */
+int alipmpc_solve_launches(void* handle, int64_t B, int32_t* launches, int32_t* team);
 
 /* The device program this handle's solves run (cfg.program): "solve_kernel<N,rows/4,type>" (one instance per
  * wavefront; launched as one wave per instance when the batch fits alipmpc_solve_slots, as the persistent

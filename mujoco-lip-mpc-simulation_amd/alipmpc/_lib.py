@@ -40,7 +40,7 @@ class Cfg(ctypes.Structure):
 EXPORTS = ("alipmpc_default_cfg", "alipmpc_rows_per_step", "alipmpc_num_vars", "alipmpc_create",
            "alipmpc_solve_batch", "alipmpc_eval_batch", "alipmpc_rollout_batch", "alipmpc_closed_loop_batch",
            "alipmpc_trace_len",
-           "alipmpc_trace_batch", "alipmpc_nominal_gait_batch", "alipmpc_solve_slots", "alipmpc_solve_program", "alipmpc_last_kernel_ms",
+           "alipmpc_trace_batch", "alipmpc_nominal_gait_batch", "alipmpc_solve_slots", "alipmpc_solve_launches", "alipmpc_solve_program", "alipmpc_last_kernel_ms",
            "alipmpc_build_id",
            "alipmpc_last_error", "alipmpc_destroy")
 
@@ -95,6 +95,10 @@ def load(build_if_missing=True):
     if hasattr(L, "alipmpc_nominal_gait_batch"):   # (absent from older dev builds used for A/B timing)
         L.alipmpc_nominal_gait_batch.argtypes = [P, ctypes.c_int64, ctypes.c_double, P, P, P, P, P, P]
         L.alipmpc_nominal_gait_batch.restype = ctypes.c_int
+    if hasattr(L, "alipmpc_solve_launches"):
+        L.alipmpc_solve_launches.argtypes = [P, ctypes.c_int64, ctypes.POINTER(ctypes.c_int32),
+                                             ctypes.POINTER(ctypes.c_int32)]
+        L.alipmpc_solve_launches.restype = ctypes.c_int
     if hasattr(L, "alipmpc_solve_slots"):     # (absent from older dev builds used for A/B timing)
         L.alipmpc_solve_slots.argtypes = [P, ctypes.POINTER(ctypes.c_int64)]
         L.alipmpc_solve_slots.restype = ctypes.c_int
@@ -216,6 +220,14 @@ class Solver:
         v = ctypes.c_int64(0)
         self._check(self._L.alipmpc_solve_slots(self._h, ctypes.byref(v)), "alipmpc_solve_slots")
         return int(v.value)
+
+    def solve_launches(self, B):
+        """(kernel launches per solve of B instances, phase-2 team size) — 2 for a split launch
+        (include/alipmpc.h: alipmpc_solve_launches)."""
+        n, t = ctypes.c_int32(0), ctypes.c_int32(0)
+        self._check(self._L.alipmpc_solve_launches(self._h, int(B), ctypes.byref(n), ctypes.byref(t)),
+                    "alipmpc_solve_launches")
+        return int(n.value), int(t.value)
 
     # ---------------------------------------------------------------- host (numpy) calls
     def _inputs(self, x0, goal, leg, cir, nc, elp, ne):

@@ -87,8 +87,14 @@ struct KP {
     int ckpt_it;            // split launch, phase 1 (> 0): an instance still running at this iteration saves its
                             // loop state to a record and stops (solve_kernel, one wave per instance)
     int resume;             // split launch, phase 2: wave k resumes the instance of record k
+    int ckpt_tr;            // split launch, phase 1 (> 0, with team > 0): an instance whose line search has run this
+                            // many trials also stops (before ckpt_it) and gets a TEAM record
+    int team;               // split launch (team-capable build): phase 1 — team records on (ckpt_tr); phase 2 — team
+                            // workgroups ahead of the single ones (each runs one team record on its 4 waves in lockstep,
+                            // consecutive line-search trials per round)
     double* ckpt;           // split launch: per-record loop state (ckpt_doubles(RPL) each)
-    uint32_t* cont;         // split launch: cont[0] = records written, cont[1 + k] = instance of record k
+    uint32_t* cont;         // split launch counters (CONT_*): single / team records, then the instance of record k
+                            // (singles from k = 0 up, team record j at k = B - 1 - j)
     // solve outputs
     double* u_out;
     double* foot_out;
@@ -119,6 +125,13 @@ __host__ __device__ constexpr int ckpt_doubles(int rpl) { return WAVE * (CKPT_RO
 #define ALIP_SPLIT_IT 16
 #endif
 constexpr int SPLIT_IT_DEFAULT = ALIP_SPLIT_IT;   // phase-1 iteration cap of the split launch (launch_solve)
+constexpr int SPLIT_TR_DEFAULT = 0;               // phase-1 trial cut of a cold solve (0 = off: no team records)
+constexpr int CL_SPLIT_IT_DEFAULT = 16;           // the closed loop's per-tick solves: phase-1 cap
+constexpr int CL_SPLIT_TR_DEFAULT = 40;           // and trial cut
+// split-launch counters (KP.cont): single records, team records, then the B instance ids of records (index k)
+constexpr int CONT_SINGLE = 0, CONT_TEAM = 1;
+__host__ __device__ constexpr long long cont_hdr(long long) { return 2; }
+constexpr long long TEAM_CAP = 128;   // team workgroups of a phase-2 launch (team records beyond run one wave each)
 #ifndef ALIP_GJ_REGS
 #define ALIP_GJ_REGS 1
 #endif
@@ -718,6 +731,10 @@ __device__ void prologue(const KP& P, const WT& w, const typename WT::real* G, c
 
 // 1/sqrt(d) and 1/x to ~1 ulp: hardware estimate + two Newton steps (a few FMAs instead of the
 // ~15-instruction IEEE sqrt / div sequences on the Cholesky critical path)
+// binary exponent of a normal nonzero value (the trial count of a line search from a = ap 2^-j)
+__device__ __forceinline__ int fexp2(double x) { return __builtin_amdgcn_frexp_exp(x); }
+__device__ __forceinline__ int fexp2(float x) { return __builtin_amdgcn_frexp_expf(x); }
+
 __device__ __forceinline__ double rsqrt_nr(double d)
 {
     double y = __builtin_amdgcn_rsq(d);
@@ -983,7 +1000,7 @@ struct RowK {   // uniform constants of the row functions
     R gm1, s, q, p, r, gxg, gyg;
 };
 // cst slots
-enum { K_GM1 = 0, K_S, K_Q, K_P, K_R, K_GXG, K_GYG, K_THMAX, K_THMIN, K_MACT, K_NBL, K_TOL, K_ACCTOL };
+enum { K_GM1 = 0, K_S, K_Q, K_P, K_R, K_GXG, K_GYG, K_THMAX, K_THMIN, K_MACT, K_NBL, K_TOL, K_ACCTOL, K_NTR, K_XR };
 template <class R>
 __device__ __forceinline__ RowK<R> load_rowk(const R* cst)
 {
@@ -1158,9 +1175,15 @@ __device__ __forceinline__ R obj_sum(const R (&v)[RPL], int mr4)
     return s;
 }
 
-template <int N, int KSM, class R, bool Q>
-__device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int wv, long long b, long long rec = -1)
+// TM: the team-capable build (split launches with team records, solve_kernel<..., TM = true>): phase 1 also cuts an
+// instance by its line-search trial count, phase 2 runs team records on 4 waves; tm < 0 = member -1 - tm of a team.
+// Without TM all of it compiles out: the interior-point loop of the plain build sits at its register budget, and the
+// team logic in the same body had cost 36 -> 172 B/lane of spills (the register allocator, not the arithmetic).
+template <int N, int KSM, class R, bool Q, bool TM = false>
+__device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int wv, long long b, long long rec = -1,
+                                          int tm = 0)
 {
+    if constexpr (!TM) tm = 0;
     // Q (persistent instance loop): opaque per-instance copies of the lane-/wave-derived inputs, so that
     // nothing computed from them is loop-invariant and no address or row table is hoisted out of the
     // instance loop (and spilled).  (Laundering the LDS base offsets as well cut the scratch further but
@@ -1192,6 +1215,8 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
     WSTAMP_DECL
     WSS<N, R> w = carve_s<N, R>(wsb + (size_t)wv * wss_elems<N, R>(nc_max, ne_max, mr4, mo4), nc_max, ne_max, mr4, mo4);
     for (int i = lane; i < 64 * (N + 1); i += WAVE) w.S[i] = R(0.0);
+    // tm < 0: member -1 - tm of a team (team-capable build).  The line-search trial count (phase 1's trial cut,
+    // w.cst[K_NTR]) and a team's exchange-round parity (w.cst[K_XR]) live in LDS, not in loop-carried registers
 
     double gxg, gyg, uj;
     int legv;
@@ -1238,6 +1263,8 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
         }                               \
     } while (0)
     if (lane == 0) {
+        w.cst[K_NTR] = R(0.0);
+        w.cst[K_XR] = R(0.0);
         w.cst[K_GM1] = P.gm1; w.cst[K_S] = P.s; w.cst[K_Q] = P.q; w.cst[K_P] = P.p; w.cst[K_R] = P.r;
         w.cst[K_GXG] = gxg; w.cst[K_GYG] = gyg; w.cst[K_TOL] = P.tol; w.cst[K_ACCTOL] = P.acc_tol;
     }
@@ -1377,15 +1404,22 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
             __builtin_amdgcn_s_setprio(1);
 #endif
     }
-    const int ckpt_it = rfl(P.ckpt_it);
 
+    // phase-1 cuts (a team's own solve is never cut)
+    const int ckpt_it = TM && tm < 0 ? 0 : rfl(P.ckpt_it);
+    const int ckpt_tr = TM && tm >= 0 ? rfl(P.team > 0 ? P.ckpt_tr : 0) : 0;
     STAMP_DECL
     for (it = it0; it <= max_iter; ++it) {
         // split launch, phase 1: an instance still running at iteration ckpt_it writes its loop state to the next
-        // record and stops; phase 2 resumes it on a wave of its own (the long instances no longer share SIMDs)
-        if (ckpt_it > 0 && it == ckpt_it) {
+        // record and stops; phase 2 resumes it on a wave of its own (the long instances no longer share SIMDs).
+        // Team-capable build: an instance whose line searches have run ckpt_tr trials (a long search every
+        // iteration) stops early and writes a TEAM record, which phase 2 resumes on a workgroup's 4 waves
+        if ((ckpt_it > 0 && it == ckpt_it) || (TM && ckpt_tr > 0 && w.cst[K_NTR] >= R(ckpt_tr))) {
+            const bool to_team = TM && !(ckpt_it > 0 && it == ckpt_it);
             int k = 0;
-            if (lane == 0) k = (int)atomicAdd(P.cont, 1u);
+            if (lane == 0)
+                k = to_team ? (int)(P.B - 1 - (long long)atomicAdd(P.cont + CONT_TEAM, 1u))
+                            : (int)atomicAdd(P.cont + CONT_SINGLE, 1u);
             k = rfl(k);
             double* rc = P.ckpt + (long long)k * ckpt_doubles(RPL);
 #pragma unroll
@@ -1415,7 +1449,7 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
 #pragma unroll
             for (int i = 0; i < 11; ++i) v = lane == i ? sv[i] : v;
             if (lane < 11) rc[WAVE * (CKPT_ROW * RPL + 5) + lane] = v;
-            if (lane == 0) P.cont[1 + k] = (uint32_t)b;
+            if (lane == 0) P.cont[cont_hdr(P.B) + k] = (uint32_t)b;
             status = ST_CKPT;
             break;
         }
@@ -1809,66 +1843,130 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
         amin = uni(amin * gal);
         STAMP(6);
         // ---- filter line search on trial points V + a dV (row registers only)
+        // Trial j is a_j = ap 2^-j (and log a_j by the same sequential subtractions); the search takes the first
+        // acceptable trial with a_j >= amin.  A team (4 waves in lockstep on one instance, team-capable build)
+        // evaluates trials J + member in one round, exchanges accept flags through LDS, and every member other than
+        // the first accepting one re-evaluates that trial: the same trials, the same arithmetic, the same choice as one
+        // wave.
         R a = ap;
         R la = uni(llog(ap));   // log a, tracked exactly through the halvings
         bool accepted = false, ftype = false;
         R ctr[RPL], ta0[RPL], ta1[RPL];
         R ft = R(0.0), lgt = R(0.0), tht_acc = R(0.0);
-        while (a >= amin) {
-            WSTAMP_TRIAL;
-            RELANE();
-            R tht = R(0.0);
-            ft = R(0.0);
-            lgt = R(0.0);
-            bool bad = false;
-#pragma unroll
-            for (int q = 0; q < RPL; ++q) {
-                // the trial point is rebuilt from (rv, rdv, a) where needed (on acceptance, the same fma)
-                R vt[4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) vt[i] = fma(a, rdv[q][i], rv[q][i]);
-                R o[6];
-#pragma unroll
-                for (int i = 0; i < 6; ++i) o[i] = w.obs6[6 * roi[q] + i];
-                row_trans(rtype[q], vt, w.cst[K_GXG], w.cst[K_GYG], ta0[q], ta1[q]);
-                ctr[q] = row_value(rtype[q], rk[q], vt, ta0[q], ta1[q], o, CK);
-                const R st = sr[q] + a * dS[q];
-                if (rtype[q] < R_NONE) tht += fabs(ctr[q] - st);
-
-                const R d1 = st - cl[q], d2 = cu[q] - st;
-                if (HL(q) && !(d1 > 0)) bad = true;
-                if (HU(q) && !(d2 > 0)) bad = true;
-                lgt += HL(q) ? (HU(q) ? llog(d1 * d2) : llog(d1)) : (HU(q) ? llog(d2) : R(0.0));
-            }
-            tht = wsum(tht);
-            ft = obj_sum<N, RPL>(ctr, mr4);
-            lgt = wsum(lgt);
-            const bool anybad = __ballot(bad) != 0ull;
-            const R pht = anybad ? INFINITY : ft - mu * lgt;
-            bool ok = isfinite(pht) && tht < w.cst[K_THMAX];
-            if (ok) {
-                const bool b0 = lane < nf && !(tht < fth0 || pht < fph0);
-                const bool b1 = lane + WAVE < nf && !(tht < fth1 || pht < fph1);
-                ok = __ballot(b0 || b1) == 0ull;
-            }
-            if (ok) {
-                const bool switching = gphi < 0 && la > lsw;
-                if (switching && theta <= w.cst[K_THMIN]) {
-                    if (pht <= phi + eta * a * gphi) {
-                        accepted = true;
-                        ftype = true;
-                    }
-                } else if (tht <= (1 - gth) * theta || pht <= phi - gph * theta) {
-                    accepted = true;
-                    ftype = false;
+        bool redo = false;   // team: this pass re-evaluates the winning trial (a, la already advanced to it)
+        for (;;) {
+            R am = a, lam = la;   // this member's trial
+            if (!(TM && redo))
+                for (int t = 0; t < -1 - tm; ++t) {
+                    am = uni(am * R(0.5));
+                    lam = uni(lam - R(M_LN2));
                 }
+            const bool valid = am >= amin;
+            bool acc_m = false, fty_m = false;
+            if (valid) {
+                WSTAMP_TRIAL;
+                RELANE();
+                R tht = R(0.0);
+                ft = R(0.0);
+                lgt = R(0.0);
+                bool bad = false;
+#pragma unroll
+                for (int q = 0; q < RPL; ++q) {
+                    // the trial point is rebuilt from (rv, rdv, a) where needed (on acceptance, the same fma)
+                    R vt[4];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) vt[i] = fma(am, rdv[q][i], rv[q][i]);
+                    R o[6];
+#pragma unroll
+                    for (int i = 0; i < 6; ++i) o[i] = w.obs6[6 * roi[q] + i];
+                    row_trans(rtype[q], vt, w.cst[K_GXG], w.cst[K_GYG], ta0[q], ta1[q]);
+                    ctr[q] = row_value(rtype[q], rk[q], vt, ta0[q], ta1[q], o, CK);
+                    const R st = sr[q] + am * dS[q];
+                    if (rtype[q] < R_NONE) tht += fabs(ctr[q] - st);
+
+                    const R d1 = st - cl[q], d2 = cu[q] - st;
+                    if (HL(q) && !(d1 > 0)) bad = true;
+                    if (HU(q) && !(d2 > 0)) bad = true;
+                    lgt += HL(q) ? (HU(q) ? llog(d1 * d2) : llog(d1)) : (HU(q) ? llog(d2) : R(0.0));
+                }
+                tht = wsum(tht);
+                ft = obj_sum<N, RPL>(ctr, mr4);
+                lgt = wsum(lgt);
+                const bool anybad = __ballot(bad) != 0ull;
+                const R pht = anybad ? INFINITY : ft - mu * lgt;
+                bool ok = isfinite(pht) && tht < w.cst[K_THMAX];
+                if (ok) {
+                    const bool b0 = lane < nf && !(tht < fth0 || pht < fph0);
+                    const bool b1 = lane + WAVE < nf && !(tht < fth1 || pht < fph1);
+                    ok = __ballot(b0 || b1) == 0ull;
+                }
+                if (ok) {
+                    const bool switching = gphi < 0 && lam > lsw;
+                    if (switching && theta <= w.cst[K_THMIN]) {
+                        if (pht <= phi + eta * am * gphi) {
+                            acc_m = true;
+                            fty_m = true;
+                        }
+                    } else if (tht <= (1 - gth) * theta || pht <= phi - gph * theta) {
+                        acc_m = true;
+                        fty_m = false;
+                    }
+                }
+                tht_acc = tht;
             }
-            tht_acc = tht;
-            if (accepted) break;
-            a = uni(a * R(0.5));
-            la = uni(la - R(M_LN2));
+            if (TM && redo) {   // the winner's trial values are this member's now
+                accepted = true;
+                break;
+            }
+            if (!TM || tm >= 0) {
+                if (!valid) break;
+                if (acc_m) {
+                    accepted = true;
+                    ftype = fty_m;
+                    break;
+                }
+                a = uni(a * R(0.5));
+                la = uni(la - R(M_LN2));
+                continue;
+            }
+            // team round: member m's accept flag for round parity p sits in m's own per-instance constants
+            // (cst[15] / cst[K_NTR]: no trial cut in a team); a member's next write to a parity follows the
+            // barrier that every reader of the previous one passes first
+            if constexpr (!TM) break;
+            {
+                const int me = -1 - tm;
+                const int wss = wss_elems<N, R>(rfl(P.nc_max), rfl(P.ne_max), rfl(P.mr4), rfl(P.mo4));
+                const int par = w.cst[K_XR] != R(0.0) ? 1 : 0;
+                const int fsl = par ? K_NTR : 15;
+                if (lane == 0) {
+                    w.cst[fsl] = R(valid ? (acc_m ? (fty_m ? 3 : 2) : 1) : 0);
+                    w.cst[K_XR] = R(1 - par);
+                }
+                __syncthreads();
+                const R* cst0 = w.cst - me * wss;   // member 0's constants
+                int wn = 0, fw = 0;   // first member whose trial did not end in a rejection, and its flag
+                for (; wn < 4; ++wn) {
+                    fw = rfl((int)cst0[wn * wss + fsl]);
+                    if (fw != 1) break;
+                }
+                for (int t = 0; t < wn; ++t) {   // a, la of trial J + wn (J + 4 when all four rejected)
+                    a = uni(a * R(0.5));
+                    la = uni(la - R(M_LN2));
+                }
+                if (wn == 4) continue;
+                if (fw == 0) break;   // trial J + wn is below amin: no acceptable trial
+                ftype = fw == 3;
+                if (wn == me) {
+                    accepted = true;
+                    break;
+                }
+                redo = true;
+            }
         }
         STAMP(7);
+        // trials of this search (a = ap 2^-j: j + 1 evaluated when trial j was taken, j when a fell below amin)
+        if (TM && ckpt_tr > 0 && lane == 0)
+            w.cst[K_NTR] += R(fexp2(ap) - fexp2(a) + (accepted ? 1 : 0));
         RELANE();
         if (accepted) {
             if (!ftype && nf < FILTER_CAP) {
@@ -1998,6 +2096,7 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
         else if (viol > R(1e-4))
             status = 2;
     }
+    if (TM && tm < -1) return;   // team members 1..3 computed the same outputs as member 0 (tm = -1)
     WSTAMP_WRITE(rec >= 0 ? P.B + rec : b, it, n_rest);   // (diagnostic build: phase-2 records after the batch's)
     // canonical u: u_k = x_{k+1} (W u_k = p_k since W B = I) — the reference's "desired next state"
     if (lane < 5 * N) P.u_out[(size_t)b * 5 * N + lane] = w.V[gx(lane / 5 + 1, lane % 5)];
@@ -2059,7 +2158,7 @@ constexpr int solve_waves() { return 4 * KSM > WAVE ? ALIP_WAVES_RPL2 : (sizeof(
 // solve_one and produce the same bits for an instance (test_work_queue_batch_independence solves a batch
 // above the slots whole and in half-slot chunks and compares status, iters, u, foot, x_pred exactly), so an
 // instance's result does not depend on its batch or on the device's slot count.
-template <int N, int KSM, class R, bool ONE>
+template <int N, int KSM, class R, bool ONE, bool TM = false>
 __global__ __launch_bounds__(256, (solve_waves<KSM, R>())) void solve_kernel(KP Pv)
 {
     using D = Dim<N>;
@@ -2079,21 +2178,33 @@ __global__ __launch_bounds__(256, (solve_waves<KSM, R>())) void solve_kernel(KP 
     // slot k of the launch (wave k, or the k-th queue ticket) solves instance order[k] (identity without an order):
     // the per-instance arithmetic does not depend on the slot, only when and where the instance runs
     if constexpr (ONE) {
-        const long long k = (long long)blockIdx.x * WAVES_PER_BLOCK + wv;
-        long long b = -1, rec = -1;   // one inlined solve_one for both forms (the code is large)
-        if (Pv.resume) {   // split launch, phase 2: wave k finishes the instance of record k
-            const long long cnt = (long long)__builtin_amdgcn_readfirstlane(Pv.cont[0]);
-            if (k < cnt) {
-                b = (long long)__builtin_amdgcn_readfirstlane(Pv.cont[1 + k]);
-                rec = k;
+        // split phase 2 of the team-capable build: workgroups [0, Pv.team) resume team records (the workgroup's 4 waves
+        // in lockstep on one instance), the rest single records one wave each, then any team records beyond Pv.team
+        const long long nteamwg = TM && Pv.resume ? (long long)Pv.team : 0;
+        const bool team = (long long)blockIdx.x < nteamwg;
+        const long long k = team ? (long long)blockIdx.x : ((long long)blockIdx.x - nteamwg) * WAVES_PER_BLOCK + wv;
+        long long b = -1, rec = -1;   // one inlined solve_one for every form (the code is large)
+        if (Pv.resume) {   // split launch, phase 2
+            const long long made = TM ? (long long)__builtin_amdgcn_readfirstlane(Pv.cont[CONT_TEAM]) : 0;
+            if (team) {
+                if (k < made) rec = Pv.B - 1 - k;
+            } else {
+                const long long cnt = (long long)__builtin_amdgcn_readfirstlane(Pv.cont[CONT_SINGLE]);
+                if (k < cnt)
+                    rec = k;
+                else if (k - cnt + nteamwg < made)
+                    rec = Pv.B - 1 - (k - cnt + nteamwg);
             }
+            if (rec >= 0) b = (long long)__builtin_amdgcn_readfirstlane(Pv.cont[cont_hdr(Pv.B) + rec]);
         } else if (k < Pv.B) {
             b = Pv.order ? (long long)__builtin_amdgcn_readfirstlane(Pv.order[k]) : k;
             if (Pv.active && !Pv.active[b]) b = -1;
         }
         b = __builtin_amdgcn_readfirstlane((int)b);
         rec = __builtin_amdgcn_readfirstlane((int)rec);
-        if (b >= 0) solve_one<N, KSM, R, false>(P, G, E, wsb, wv, b, rec);
+        // (one call site: the team solves run the very machine code of the single ones — two inlined copies had
+        // rounded differently)
+        if (b >= 0) solve_one<N, KSM, R, false, TM>(P, G, E, wsb, wv, b, rec, team ? -1 - wv : 0);
     } else {
         uint32_t* const q = Pv.queue;
         for (long long k = next_instance(q); k < Pv.B; k = next_instance(q)) {
@@ -4226,22 +4337,32 @@ static unsigned resident_blocks(const void* f, size_t smem, int threads = WAVE *
 template <int N, class R>
 void launch_solve(const KP& P0, size_t smem, hipStream_t st, unsigned* res_out)
 {
-    const unsigned need = (unsigned)((P0.B + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
+    // (a split phase 2 of the team-capable build: P0.team team workgroups ahead of the one-wave-per-instance ones)
+    const unsigned need = (P0.resume ? (unsigned)P0.team : 0u) + (unsigned)((P0.B + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
     // KSM = 4-row steps of the J layout, the smallest compiled size covering mo4 rows
-    auto go = [&](auto kq, auto k1) {
+    auto go = [&](auto kq, auto k1, auto kt) {
         set_smem((const void*)kq, smem);
         set_smem((const void*)k1, smem);
+        set_smem((const void*)kt, smem);
         const unsigned res = resident_blocks((const void*)kq, smem);
         if (res_out) {   // query only (alipmpc_solve_slots)
             *res_out = res;
             return;
         }
-        if (res > 0 && need > res)   // the persistent work queue over the resident workgroups
+        if (res > 0 && need > res && !P0.resume)   // the persistent work queue over the resident workgroups
             hipLaunchKernelGGL(kq, dim3(res), dim3(WAVE * WAVES_PER_BLOCK), smem, st, P0);
+        else if (P0.team > 0)        // a split launch with team records: both phases on the team-capable build
+            hipLaunchKernelGGL(kt, dim3(need > 0 ? need : 1u), dim3(WAVE * WAVES_PER_BLOCK), smem, st, P0);
         else                         // every instance has a resident wave: one instance per wave
             hipLaunchKernelGGL(k1, dim3(need > 0 ? need : 1u), dim3(WAVE * WAVES_PER_BLOCK), smem, st, P0);
     };
-#define ALIP_GO(K) go(solve_kernel<N, K, R, false>, solve_kernel<N, K, R, true>)
+    // the team-capable build exists in fp64 only: in fp32 its different code rounded differently from the plain build's
+    // (fp32 contraction / packing decisions depend on the surrounding code), so fp32 splits never make team records
+#define ALIP_GO(K) go(solve_kernel<N, K, R, false>, solve_kernel<N, K, R, true>, \
+                      solve_kernel<N, K, R, true, sizeof(R) == 8>)
+#ifdef ALIP_DEV_ONLY_KSM   // dev builds for register reports (tools/regs.py): one row-step count only
+    ALIP_GO(ALIP_DEV_ONLY_KSM);
+#else
     if (P0.mo4 <= 32)
         ALIP_GO(8);
     else if (P0.mo4 <= 40)
@@ -4256,6 +4377,7 @@ void launch_solve(const KP& P0, size_t smem, hipStream_t st, unsigned* res_out)
         ALIP_GO(32);
     else
         ALIP_GO(48);
+#endif
 #undef ALIP_GO
 }
 
@@ -4264,7 +4386,9 @@ template <int N>
 hipError_t launch_t(bool solve, bool f32, const KP& P, size_t smem, hipStream_t st, unsigned* res_out)
 {
     if (solve && f32) {
+#ifndef ALIP_DEV_ONLY_KSM
         launch_solve<N, float>(P, smem, st, res_out);
+#endif
     } else if (solve) {
         launch_solve<N, double>(P, smem, st, res_out);
     } else {
@@ -4467,6 +4591,8 @@ struct Handle {
     // split launch of the wave program (ALIPMPC_SPLIT_IT): the phase-1 iteration cap (0 = off) and, per stream, the
     // record buffer (launches on one stream run in order, so they may share it; other streams get their own)
     int split_it = 0;
+    int split_tr = 0;   // phase-1 trial cut: an instance at this many line-search trials resumes as a team (0 = off)
+    int cl_split_it = 0, cl_split_tr = 0;   // the closed loop's per-tick solves (ALIPMPC_CL_SPLIT_IT / _TR)
     struct SplitBuf {
         void* p = nullptr;
         size_t bytes = 0;
@@ -4962,6 +5088,14 @@ int alipmpc_create(const alipmpc_cfg* cfg, int device, void** handle)
             const char* se = std::getenv("ALIPMPC_SPLIT_IT");
             h->split_it = se ? std::atoi(se) : SPLIT_IT_DEFAULT;
             if (h->split_it < 0 || h->split_it >= h->cfg.max_iter) h->split_it = 0;
+            auto env_int = [](const char* name, int dflt) {
+                const char* t = std::getenv(name);
+                return t ? std::max(0, std::atoi(t)) : dflt;
+            };
+            h->split_tr = env_int("ALIPMPC_SPLIT_TR", SPLIT_TR_DEFAULT);
+            h->cl_split_it = env_int("ALIPMPC_CL_SPLIT_IT", CL_SPLIT_IT_DEFAULT);
+            if (h->cl_split_it >= h->cfg.max_iter) h->cl_split_it = 0;
+            h->cl_split_tr = env_int("ALIPMPC_CL_SPLIT_TR", CL_SPLIT_TR_DEFAULT);
         }
         if (h->cfg.program == ALIPMPC_PROGRAM_LANE) {
             h->lane_nct = lane_slots_for(h->cfg);
@@ -4985,17 +5119,19 @@ int alipmpc_create(const alipmpc_cfg* cfg, int device, void** handle)
 // 30-iteration cap) otherwise finish at the pace of the busiest SIMDs, which hold two or three of them
 // among their four waves; in phase 2 they are few enough for a SIMD each.  Every instance executes the same
 // arithmetic either way (the record holds its exact loop state): same bits (test_split_launch_bit_identical).
-static hipError_t launch_solve(Handle* h, const KP& P, hipStream_t st)
+static hipError_t launch_solve(Handle* h, const KP& P, hipStream_t st, int split_it, int split_tr)
 {
     const alipmpc_cfg& cf = h->cfg;
-    if (cf.variant == ALIPMPC_VARIANT_DD || h->lane_nct >= 0 || h->split_it <= 0 || P.B < 2 || P.active || P.order)
+    if (cf.precision == ALIPMPC_PREC_FP32) split_tr = 0;   // (the team-capable build is fp64 only)
+    if (cf.variant == ALIPMPC_VARIANT_DD || h->lane_nct >= 0 || (split_it <= 0 && split_tr <= 0) || P.B < 2 || P.order)
         return launch(h, true, P, st);
     unsigned res = 0;
     if (hipError_t e = launch(h, true, P, st, &res)) return e;
     if ((long long)res * WAVES_PER_BLOCK < P.B) return launch(h, true, P, st);   // the work-queue form
     const size_t rpl = (size_t)((h->mo4 + WAVE - 1) / WAVE);
     const size_t rec_bytes = ((size_t)P.B * ckpt_doubles((int)rpl) * sizeof(double) + 255) & ~(size_t)255;
-    const size_t need = rec_bytes + ((size_t)P.B + 1) * sizeof(uint32_t);
+    const size_t hdr = (size_t)cont_hdr(P.B);
+    const size_t need = rec_bytes + (hdr + (size_t)P.B) * sizeof(uint32_t);
     void* buf = nullptr;
     {
         std::lock_guard<std::mutex> lk(h->split_mtx);
@@ -5013,14 +5149,18 @@ static hipError_t launch_solve(Handle* h, const KP& P, hipStream_t st)
         buf = sb.p;
     }
     uint32_t* cont = reinterpret_cast<uint32_t*>((char*)buf + rec_bytes);
-    if (hipError_t e = hipMemsetAsync(cont, 0, sizeof(uint32_t), st)) return e;
+    if (hipError_t e = hipMemsetAsync(cont, 0, hdr * sizeof(uint32_t), st)) return e;
+    const int team = split_tr > 0 ? (int)std::min<long long>(P.B, TEAM_CAP) : 0;
     KP P1 = P;
-    P1.ckpt_it = h->split_it;
+    P1.ckpt_it = split_it > 0 ? split_it : 0;
+    P1.ckpt_tr = split_tr;
+    P1.team = team;
     P1.ckpt = (double*)buf;
     P1.cont = cont;
     if (hipError_t e = launch(h, true, P1, st)) return e;
-    KP P2 = P;
+    KP P2 = P;   // single records, and team records
     P2.resume = 1;
+    P2.team = team;
     P2.ckpt = (double*)buf;
     P2.cont = cont;
     return launch(h, true, P2, st);
@@ -5056,7 +5196,7 @@ static int run_batch(Handle* h, bool solve, int64_t B, const double* x0, const d
         const int ei = h->evi;
         h->evi = (ei + 1) % Handle::NEV;
         HIPCHK(h, hipEventRecord(h->ev[ei][0], st));
-        HIPCHK(h, solve ? launch_solve(h, P, st) : launch(h, false, P, st));
+        HIPCHK(h, solve ? launch_solve(h, P, st, h->split_it, h->split_tr) : launch(h, false, P, st));
         HIPCHK(h, hipEventRecord(h->ev[ei][1], st));
         h->evlast = ei;
         h->timed = true;
@@ -5138,7 +5278,7 @@ static int run_batch(Handle* h, bool solve, int64_t B, const double* x0, const d
     const int ei = h->evi;
     h->evi = (ei + 1) % Handle::NEV;
     HIPCHK(h, hipEventRecord(h->ev[ei][0], st));
-    HIPCHK(h, solve ? launch_solve(h, P, st) : launch(h, false, P, st));
+    HIPCHK(h, solve ? launch_solve(h, P, st, h->split_it, h->split_tr) : launch(h, false, P, st));
     HIPCHK(h, hipEventRecord(h->ev[ei][1], st));
     h->evlast = ei;
     h->timed = true;
@@ -5448,7 +5588,7 @@ int alipmpc_closed_loop_batch(void* handle, int64_t B, int32_t S, int32_t f_cyc,
                 HIPCHK(h, hipStreamSynchronize(st));   // &base is a stack value
             }
 #endif
-            HIPCHK(h, launch(h, true, P, st));
+            HIPCHK(h, launch_solve(h, P, st, h->cl_split_it, h->cl_split_tr));
             hipLaunchKernelGGL(cl_update_kernel, dim3(g1), dim3(256), 0, st, C);
             HIPCHK(h, hipGetLastError());
         }
@@ -5654,6 +5794,20 @@ int alipmpc_solve_slots(void* handle, int64_t* slots)
         *slots = (int64_t)res * (h->cfg.precision == ALIPMPC_PREC_FP32 ? lane::lanes_of<float>() : lane::lanes_of<double>());
     else
         *slots = (int64_t)res * WAVES_PER_BLOCK;
+    return ALIPMPC_OK;
+}
+
+int alipmpc_solve_launches(void* handle, int64_t B, int32_t* launches, int32_t* team)
+{
+    Handle* h = (Handle*)handle;
+    if (!h || !launches || !team) return fail(h, ALIPMPC_EINVAL, "null argument");
+    int64_t slots = 0;
+    if (int rc = alipmpc_solve_slots(handle, &slots)) return rc;
+    // launch_solve's conditions for the split form (no order / active mask on the batch API)
+    const bool split = h->cfg.variant != ALIPMPC_VARIANT_DD && h->lane_nct < 0 && h->split_it > 0 && B >= 2 &&
+                       B <= slots;
+    *launches = split ? 2 : 1;
+    *team = split && h->split_tr > 0 && h->cfg.precision != ALIPMPC_PREC_FP32 ? 4 : 1;
     return ALIPMPC_OK;
 }
 

@@ -1162,13 +1162,49 @@ def test_split_launch_bit_identical(gpu_lib, variant, N, n_cir, n_elp, prec, B, 
     cfg = gpu_lib.default_cfg(variant, N, **kw)
     outs = {}
     for k in ("0", "1", "7", "16", str(cfg.max_iter - 1)):
-        monkeypatch.setenv("ALIPMPC_SPLIT_IT", k)
-        s = gpu_lib.Solver(cfg)
-        assert s.solve_slots() >= B
-        outs[k] = s.solve(bt["x0"], bt["goal"], bt["leg"], bt["cir"], bt["nc"], bt.get("elp"), bt.get("ne"),
-                          u0=bt["u0"])
-    ref = outs.pop("0")
+        # phase 2 one wave per instance, and with team records (ALIPMPC_SPLIT_TR: an instance at that many
+        # line-search trials is cut early and resumes on a team, the workgroup's 4 waves in lockstep, consecutive
+        # trials per round)
+        for tr in (("0", "3", "12") if k != "0" else ("0",)):
+            monkeypatch.setenv("ALIPMPC_SPLIT_IT", k)
+            monkeypatch.setenv("ALIPMPC_SPLIT_TR", tr)
+            s = gpu_lib.Solver(cfg)
+            assert s.solve_slots() >= B
+            outs[k + "/" + tr] = s.solve(bt["x0"], bt["goal"], bt["leg"], bt["cir"], bt["nc"], bt.get("elp"),
+                                         bt.get("ne"), u0=bt["u0"])
+    ref = outs.pop("0/0")
     assert (ref["iters"] > 16).sum() > 0 and (ref["status"] == 2).sum() > 0
     for k, o in outs.items():
         for key in ref:
             assert np.array_equal(o[key], ref[key]), (k, key)
+
+
+@pytest.mark.parametrize("variant,kick,B,prec", [(0, 0.0, 3000, 0), (1, 0.05, 3000, 0), (0, 0.0, 4096, 1)])
+def test_closed_loop_split_team_bit_identical(gpu_lib, variant, kick, B, prec, monkeypatch):
+    """The closed loop's per-tick solves run as split launches (ALIPMPC_CL_SPLIT_IT: phase-1 cap, then the
+    unfinished instances resume from their records; ALIPMPC_CL_SPLIT_TR: an instance at that many line-search trials
+    is cut early and resumes as a team of 4 waves that evaluates consecutive trials in one round).  Stopped episodes are skipped in phase 1 and never recorded.  Every
+    output equals the one-phase loop's (ALIPMPC_CL_SPLIT_IT=0) bit for bit."""
+    from alipmpc import scenes
+    S, F = 2, 40
+    bt = scenes.make_batch(B, seed=710 + variant + 3 * prec, n_cir=5)
+    x0 = bt["x0"].copy()
+    x0[:300, 0:2] = bt["goal"][:300] - np.array([0.6, 0.5])
+    leg = bt["leg"].astype(np.int8)
+    kw = dict(nc_max=5, ne_max=0)
+    if prec:
+        kw["precision"] = gpu_lib.PREC_FP32
+    cfg = gpu_lib.default_cfg(variant, 3, **kw)
+    s0 = gpu_lib.Solver(cfg)
+    foot0 = s0.solve(x0, bt["goal"], leg, bt["cir"], bt["nc"], u0=np.tile(x0, (1, 3)))["foot"][:, 0:2]
+    outs = {}
+    for cut, tr in (("0", "0"), ("16", "40"), ("3", "0"), ("8", "5")):
+        monkeypatch.setenv("ALIPMPC_CL_SPLIT_IT", cut)
+        monkeypatch.setenv("ALIPMPC_CL_SPLIT_TR", tr)
+        outs[cut + "/" + tr] = gpu_lib.Solver(cfg).closed_loop(x0, foot0, bt["goal"], leg, bt["cir"], bt["nc"],
+                                                               steps=S, f_cyc=F, kick=kick, seed=3)
+    ref = outs.pop("0/0")
+    assert (ref["status"] == 2).sum() > 0 and (ref["steps_to_goal"] > 0).sum() > 0
+    for name, o in outs.items():
+        for k in ref:
+            assert np.array_equal(o[k], ref[k], equal_nan=True), (name, k)

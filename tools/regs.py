@@ -5,7 +5,7 @@ import sys
 import os
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SRC = os.path.join(ROOT, "mujoco-lip-mpc-simulation_amd", "csrc", "alipmpc.hip")
+SRC = os.environ.get("REGS_SRC") or os.path.join(ROOT, "mujoco-lip-mpc-simulation_amd", "csrc", "alipmpc.hip")
 cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-mllvm", "-disable-machine-licm",
        "-Wno-unused-value", "--cuda-device-only", "-c", "-o", "/tmp/alipmpc_regs.o", SRC,
        "-Rpass-analysis=kernel-resource-usage"] + sys.argv[1:]

@@ -12,7 +12,8 @@ The directory holds what tools/gpu_run.sh's `prof` step collects for ONE bench c
 Every record carries the alipmpc_build_id of the profiled library (bench.json config.build_id); bench.py attaches a
 record to its line only when that id equals the id of the library it is timing.
 
-Fields (per launch of the dominant solve kernel; the first dispatch of every pass is the warmup and skipped):
+Fields (per solve of the dominant solve kernel — a split launch's two dispatches summed, config.launches_per_solve; the
+first solve of every pass is the warmup and skipped):
   kernel_ms          kernel-trace average duration (the bench's own HIP-event figure must agree)
   achieved / frac    algorithmic FP64 flops per launch (flops_per_iter x instance-iterations) / kernel_ms, / peak
   traffic            HBM bytes: 2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md: FETCH_SIZE counts half the
@@ -49,11 +50,13 @@ def counters(d, kern, skip=1):
     return {k: sum(v) / len(v) for k, v in acc.items()}, meta
 
 
-def kernel_ms(d, kern):
+def kernel_ms(d, kern, launches=1):
+    """Mean duration per SOLVE of the kernel family: launches per solve x the mean dispatch (a split launch runs
+    phase 1 and phase 2 of every solve as two dispatches of the same kernel)."""
     for f in glob.glob(os.path.join(d, "prof_kt", "*kernel_stats.csv")):
         for r in csv.DictReader(open(f)):
             if r["Name"].startswith(kern):
-                return float(r["AverageNs"]) * 1e-6, int(r["Calls"])
+                return launches * float(r["AverageNs"]) * 1e-6, int(r["Calls"])
     return None, 0
 
 
@@ -105,10 +108,14 @@ def main():
     kname = rl["kernel"]
     kern = "void alip::" + kname.replace(",", ", ") if not kname.startswith("void") else kname
     kern = kern[:-1] if kern.endswith(">") else kern   # the family: solve_kernel<..., true/false> (launch form)
-    c, meta = counters(a.dir, kern)
-    ms, calls = kernel_ms(a.dir, kern)
+    # per-solve figures: counters of the launches of one solve summed (first solve = warmup, skipped)
+    launches = int(bench["config"].get("launches_per_solve", 1))
+    c, meta = counters(a.dir, kern, skip=launches)
+    c = {k: v * launches for k, v in c.items()}
+    ms, calls = kernel_ms(a.dir, kern, launches)
     its = rl["iters_per_launch"]
     out = {"kernel": kname, "B": bench["config"]["batch_per_gpu"], "N": bench["config"]["horizon"],
+           "launches_per_solve": launches,
            "dtype": bench["dtype"], "build_id": bench["config"].get("build_id"), "profile_dir": a.dir,
            "kernel_ms_trace": ms, "trace_calls": calls, "kernel_ms_bench": rl["kernel_ms"]}
     if ms:
