@@ -1929,24 +1929,23 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
                 la = uni(la - R(M_LN2));
                 continue;
             }
-            // team round: member m's accept flag for round parity p sits in m's own per-instance constants
-            // (cst[15] / cst[K_NTR]: no trial cut in a team); a member's next write to a parity follows the
-            // barrier that every reader of the previous one passes first
+            // team round: member m's accept flag for round parity p sits in m's own workspace (Vt[p]: prologue
+            // scratch, free afterwards); a member's next write to a parity follows the barrier that every reader of
+            // the previous one passes first
             if constexpr (!TM) break;
             {
                 const int me = -1 - tm;
                 const int wss = wss_elems<N, R>(rfl(P.nc_max), rfl(P.ne_max), rfl(P.mr4), rfl(P.mo4));
                 const int par = w.cst[K_XR] != R(0.0) ? 1 : 0;
-                const int fsl = par ? K_NTR : 15;
                 if (lane == 0) {
-                    w.cst[fsl] = R(valid ? (acc_m ? (fty_m ? 3 : 2) : 1) : 0);
+                    w.Vt[par] = R(valid ? (acc_m ? (fty_m ? 3 : 2) : 1) : 0);
                     w.cst[K_XR] = R(1 - par);
                 }
                 __syncthreads();
-                const R* cst0 = w.cst - me * wss;   // member 0's constants
+                const R* vt0 = w.Vt - me * wss;   // member 0's flags
                 int wn = 0, fw = 0;   // first member whose trial did not end in a rejection, and its flag
                 for (; wn < 4; ++wn) {
-                    fw = rfl((int)cst0[wn * wss + fsl]);
+                    fw = rfl((int)vt0[wn * wss + par]);
                     if (fw != 1) break;
                 }
                 for (int t = 0; t < wn; ++t) {   // a, la of trial J + wn (J + 4 when all four rejected)

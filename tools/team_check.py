@@ -18,7 +18,7 @@ leg = bt["leg"].astype(np.int8)
 cfg = alipmpc.default_cfg(0, 3, nc_max=5, ne_max=0)
 foot0 = alipmpc.Solver(cfg).solve(x0, bt["goal"], leg, bt["cir"], bt["nc"], u0=np.tile(x0, (1, 3)))["foot"][:, 0:2]
 ref = None
-for cut, tr in (("0", "0"), ("16", "0"), ("0", "40"), ("16", "40"), ("0", "1000"), ("0", "12"), ("0", "0")):
+for cut, tr in (("0", "0"), ("16", "0"), ("0", "40"), ("16", "40"), ("0", "1000"), ("0", "12"), ("8", "5"), ("0", "0")):
     os.environ["ALIPMPC_CL_SPLIT_IT"], os.environ["ALIPMPC_CL_SPLIT_TR"] = cut, tr
     o = alipmpc.Solver(cfg).closed_loop(x0, foot0, bt["goal"], leg, bt["cir"], bt["nc"], steps=S, f_cyc=F, seed=3)
     if ref is None:
