@@ -687,8 +687,7 @@ def test_unconverged_iterates_track_oracle(gpu_lib, coracle):
     """The reference uses the iterate as its plan whatever IPOPT's status (main_sim_mpc.py:117-121), so
     instances that end with status 2 (infeasible) or -1 (iteration cap) are compared too: the GPU runs
     the oracle's algorithm, and its last iterate lands near the oracle's on most such instances (their
-    trajectories are not contracting, so rounding-level differences can grow: a looser bar than the
-    converged one)."""
+    trajectories are not contracting, so rounding-level differences can grow on a few of them)."""
     from alipmpc import scenes
     bt = scenes.make_batch(4096, seed=0, n_cir=5)
     s = gpu_lib.Solver(gpu_lib.default_cfg(0, nc_max=5, ne_max=0))
@@ -698,8 +697,14 @@ def test_unconverged_iterates_track_oracle(gpu_lib, coracle):
     assert unc.sum() >= 100
     assert (o["status"][unc] == ref["status"][unc]).mean() >= 0.9
     err = np.abs(o["foot"] - ref["foot"]).max(axis=1)[unc]
-    assert np.mean(err <= 1e-4 * np.maximum(1.0, np.abs(ref["foot"][unc]).max(axis=1))) >= 0.7, \
+    _artifact("unconverged_iterates.json",
+              {"instances": int(unc.sum()), "status_agree": float((o["status"][unc] == ref["status"][unc]).mean()),
+               "foot_le_1e-4": float(np.mean(err <= 1e-4)), "foot_le_1e-6": float(np.mean(err <= 1e-6)),
+               "foot_le_1e-9": float(np.mean(err <= 1e-9)), "foot_median": float(np.median(err))})
+    # (measured on MI355X, profiles/r3/parity: 99.8 % within 1e-4, 99.4 % within 1e-6, median 3e-15)
+    assert np.mean(err <= 1e-4 * np.maximum(1.0, np.abs(ref["foot"][unc]).max(axis=1))) >= 0.95, \
         np.mean(err <= 1e-4)
+    assert np.mean(err <= 1e-6) >= 0.9, np.mean(err <= 1e-6)
     assert np.isfinite(o["u"]).all()
 
 
@@ -938,7 +943,15 @@ def test_closed_loop_matches_oracle(gpu_lib, coracle, variant, kick, program):
     err = np.abs(o["foot"] - ref["foot"]).max(-1)
     conv = (o["status"][:, :, -1] == 0) & (ref["status"][:, :, -1] == 0)
     assert conv.sum() >= 0.4 * B * S
+    _artifact(f"closed_loop_{variant}_{kick}_{program}.json",
+              {"converged_steps": int(conv.sum()), "foot_le_1e-3": float((err[conv] <= 1e-3).mean()),
+               "foot_le_1e-4": float((err[conv] <= 1e-4).mean()), "foot_le_1e-6": float((err[conv] <= 1e-6).mean()),
+               "foot_median": float(np.median(err[conv])), "status_agree": float((o["status"] == ref["status"]).mean()),
+               "steps_to_goal_agree": float((o["steps_to_goal"] == ref["steps_to_goal"]).mean())})
+    # (measured on MI355X, profiles/r3/parity: 0.89-0.99 of the converged touchdown footholds within 1e-4 of the
+    # oracle's, median ~2e-14; the rest are episodes that drifted after a rounding-level change of path)
     assert (err[conv] <= 1e-3).mean() >= 0.9 and np.median(err[conv]) <= 1e-6
+    assert (err[conv] <= 1e-4).mean() >= 0.85, (err[conv] <= 1e-4).mean()
     # the first step's heading inputs depend on the initial state alone
     np.testing.assert_allclose(o["hd"][:, 0], ref["hd"][:, 0], rtol=0, atol=1e-12)
     np.testing.assert_allclose(o["x"][:, 0], x0, rtol=0, atol=0)
