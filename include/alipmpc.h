@@ -21,9 +21,13 @@
  *   - The caller owns every buffer.  hip_stream == NULL: all pointers are HOST pointers; the library
  *     stages them through its own device workspace and synchronises before returning.
  *     hip_stream != NULL: all pointers are DEVICE pointers (hipMalloc / torch CUDA tensors) and the call
- *     is asynchronous on that stream (no host synchronisation, no allocation after the first call of a
- *     given batch size — graph-capturable).  ALIPMPC_STREAM_NULL selects device pointers on the null
- *     (default) stream, whose handle value is 0.
+ *     is asynchronous on that stream (no host synchronisation; graph-capturable).  The only device allocation
+ *     is the split launch's record buffer (alipmpc_solve_launches): one per stream, made by the stream's first
+ *     split solve, sized for the resident slots and kept until alipmpc_destroy — a capture on a stream that has
+ *     none yet records the one-phase form.  A captured graph uses its capture stream's buffer: replay it on that
+ *     stream (or ordered with the solves there).  At most 8 streams per handle hold one; a ninth stream takes
+ *     over the least recently used buffer no capture has used.  ALIPMPC_STREAM_NULL selects device pointers on
+ *     the null (default) stream, whose handle value is 0.
  *   - Every LIP solve launch takes one of the handle's 64 work-queue counter pairs (a ring; each pair is
  *     reset by the last wave of the launch that used it).  A solve captured into a hipGraph bakes in one
  *     pair: do not replay such a graph concurrently with itself, and keep fewer than 64 solve launches of
@@ -275,10 +279,10 @@ int alipmpc_trace_batch(void* handle, int64_t B, const double* x0, const double*
 int alipmpc_solve_slots(void* handle, int64_t* slots);
 
 /* Kernel launches one alipmpc_solve_batch of B instances runs on this handle: 2 for a split launch (wave program,
- * 2 <= B <= alipmpc_solve_slots, ALIPMPC_SPLIT_IT > 0: phase 1 up to that many iterations, phase 2 resumes the
- * unfinished instances from their exact loop-state records), 1 otherwise; *team = 4 when phase 1 also cuts instances
- * by their line-search trial count (ALIPMPC_SPLIT_TR > 0, fp64 only) into team records that phase 2 runs on 4 waves
- * each, else 1.
+ * 2 <= B <= alipmpc_solve_slots, and ALIPMPC_SPLIT_IT > 0 — phase 1 up to that many iterations, phase 2 resumes the
+ * unfinished instances from their exact loop-state records — or, fp64, ALIPMPC_SPLIT_TR > 0), 1 otherwise; *team = 4
+ * when phase 1 also cuts instances by their line-search trial count (ALIPMPC_SPLIT_TR > 0, fp64 only) into team
+ * records that phase 2 runs on 4 waves each, else 1.
  * Profiling tools use it to turn per-dispatch figures into per-solve ones.  No reference counterpart. */
 int alipmpc_solve_launches(void* handle, int64_t B, int32_t* launches, int32_t* team);
 

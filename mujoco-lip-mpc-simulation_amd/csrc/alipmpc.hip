@@ -1059,7 +1059,8 @@ __device__ __forceinline__ void row_coef(int type, int k, const R (&v)[4], R a0,
     // objective
     const R w = C.q + (k == 1 ? C.p : R(0));
     const R dxg = C.gxg - v[0], dyg = C.gyg - v[1];
-    const R rho2 = dxg * dxg + dyg * dyg, ir2 = R(1) / rho2;
+    // (at p = goal exactly the target heading atan2(0, 0) = 0 is taken as locally constant: DESIGN.md §2 item 7)
+    const R rho2 = dxg * dxg + dyg * dyg, ir2 = rho2 > R(0) ? R(1) / rho2 : R(0);
     const R gp0 = -dyg * ir2, gp1 = dxg * ir2, phi = a0;
     R c0 = R(0), c1 = R(0), c2 = R(0), c3 = R(0);
     if (vel) {
@@ -2458,8 +2459,9 @@ __device__ __forceinline__ void eval_group_one(const KP& P, const GWS<N>& w, con
         const double phi = th - latan2(dyg, dxg);
         fk = wk * (ex * ex + ey * ey) + P.r * phi * phi;
         const double rho2 = dxg * dxg + dyg * dyg;
-        w.gfg[gx(k, 0)] = 2 * wk * ex + 2 * P.r * phi * (-dyg / rho2);
-        w.gfg[gx(k, 1)] = 2 * wk * ey + 2 * P.r * phi * (dxg / rho2);
+        // (p = goal exactly: the target heading's derivatives are 0)
+        w.gfg[gx(k, 0)] = 2 * wk * ex + 2 * P.r * phi * (rho2 > 0.0 ? -dyg / rho2 : 0.0);
+        w.gfg[gx(k, 1)] = 2 * wk * ey + 2 * P.r * phi * (rho2 > 0.0 ? dxg / rho2 : 0.0);
         w.gfg[gx(k, 4)] = 2 * P.r * phi;
     }
     const double f = gsum16(fk);
@@ -2743,8 +2745,8 @@ __global__ __launch_bounds__(WAVE * WPG, 2) void sweep_kernel(KP Pv)
             const double phi = th - latan2(dyg, dxg);
             fk[k] = wk * (ex * ex + ey * ey) + P.r * phi * phi;
             const double rho2 = dxg * dxg + dyg * dyg;
-            gfg[k][0] = 2 * wk * ex + 2 * P.r * phi * (-dyg / rho2);
-            gfg[k][1] = 2 * wk * ey + 2 * P.r * phi * (dxg / rho2);
+            gfg[k][0] = 2 * wk * ex + 2 * P.r * phi * (rho2 > 0.0 ? -dyg / rho2 : 0.0);
+            gfg[k][1] = 2 * wk * ey + 2 * P.r * phi * (rho2 > 0.0 ? dxg / rho2 : 0.0);
             gfg[k][2] = 2 * P.r * phi;
         }
         if (live) {
@@ -3049,7 +3051,7 @@ __device__ double dd_row(int type, int k, const double (&o)[6], const double* cs
         const double d0 = U[2 * k - 2] - up0, d1 = U[2 * k - 1] - up1;
         c = w * (dxg * dxg + dyg * dyg) + r * phi * phi + t * (d0 * d0 + d1 * d1);
         if (JAC) {
-            const double rho2 = dxg * dxg + dyg * dyg, ir2 = 1.0 / rho2;
+            const double rho2 = dxg * dxg + dyg * dyg, ir2 = rho2 > 0.0 ? 1.0 / rho2 : 0.0;   // (§2 item 7)
             const double gp0 = -dyg * ir2, gp1 = dxg * ir2;
             const double ax = -2 * w * dxg + 2 * r * phi * gp0, ay = -2 * w * dyg + 2 * r * phi * gp1, at = 2 * r * phi;
 #pragma unroll
@@ -4592,11 +4594,19 @@ struct Handle {
     int split_it = 0;
     int split_tr = 0;   // phase-1 trial cut: an instance at this many line-search trials resumes as a team (0 = off)
     int cl_split_it = 0, cl_split_tr = 0;   // the closed loop's per-tick solves (ALIPMPC_CL_SPLIT_IT / _TR)
+    // Record buffers are sized ONCE for the resident slots (the largest batch that splits) and never reallocated, so a
+    // graph captured on a stream keeps a valid pointer whatever batch sizes run on that stream later.  At most
+    // SPLIT_STREAMS of them: a further stream takes over the least recently used buffer that no capture has used
+    // (freed first); when every buffer has been captured, the new stream runs the one-phase form.
+    static constexpr size_t SPLIT_STREAMS = 8;
     struct SplitBuf {
         void* p = nullptr;
         size_t bytes = 0;
+        bool captured = false;   // used by a launch that was being captured: kept until destroy
+        unsigned long long used = 0;
     };
     std::map<hipStream_t, SplitBuf> split;
+    unsigned long long split_clock = 0;
     std::mutex split_mtx;
     // launch timing: a ring of event pairs, so a re-record never targets an event still pending on the
     // stream (that serialises the host with the previous launch)
@@ -5118,35 +5128,65 @@ int alipmpc_create(const alipmpc_cfg* cfg, int device, void** handle)
 // 30-iteration cap) otherwise finish at the pace of the busiest SIMDs, which hold two or three of them
 // among their four waves; in phase 2 they are few enough for a SIMD each.  Every instance executes the same
 // arithmetic either way (the record holds its exact loop state): same bits (test_split_launch_bit_identical).
+// whether a solve of B instances with these cuts runs as a split launch (launch_solve and alipmpc_solve_launches share
+// it): the wave program (not DD), an iteration cut or — fp64, the team-capable build — a trial cut, B within the slots
+static bool split_form(const Handle* h, long long B, int split_it, int split_tr, long long slots)
+{
+    const alipmpc_cfg& cf = h->cfg;
+    if (cf.precision == ALIPMPC_PREC_FP32) split_tr = 0;   // (the team-capable build is fp64 only)
+    return cf.variant != ALIPMPC_VARIANT_DD && h->lane_nct < 0 && (split_it > 0 || split_tr > 0) && B >= 2 &&
+           B <= slots;
+}
+
+// the stream's record buffer (Handle::split), sized for `slots` instances; nullptr: run the one-phase form
+static void* split_buffer(Handle* h, hipStream_t st, size_t need, hipError_t& err)
+{
+    err = hipSuccess;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess) return nullptr;
+    const bool capturing = cs != hipStreamCaptureStatusNone;
+    std::lock_guard<std::mutex> lk(h->split_mtx);
+    auto it = h->split.find(st);
+    if (it == h->split.end()) {
+        if (capturing) return nullptr;   // no allocation inside a capture: the one-phase form
+        if (h->split.size() >= Handle::SPLIT_STREAMS) {
+            auto lru = h->split.end();
+            for (auto j = h->split.begin(); j != h->split.end(); ++j)
+                if (!j->second.captured && (lru == h->split.end() || j->second.used < lru->second.used)) lru = j;
+            if (lru == h->split.end()) return nullptr;   // every buffer belongs to a captured graph
+            // (hipFree waits for the work in flight that may still use it)
+            if (lru->second.p) (void)hipFree(lru->second.p);
+            h->split.erase(lru);
+        }
+        Handle::SplitBuf sb;
+        if ((err = hipMalloc(&sb.p, need)) != hipSuccess) return nullptr;
+        sb.bytes = need;
+        it = h->split.emplace(st, sb).first;
+    }
+    if (it->second.bytes < need) return nullptr;   // (sized for the slots: does not happen)
+    it->second.captured |= capturing;
+    it->second.used = ++h->split_clock;
+    return it->second.p;
+}
+
 static hipError_t launch_solve(Handle* h, const KP& P, hipStream_t st, int split_it, int split_tr)
 {
     const alipmpc_cfg& cf = h->cfg;
     if (cf.precision == ALIPMPC_PREC_FP32) split_tr = 0;   // (the team-capable build is fp64 only)
-    if (cf.variant == ALIPMPC_VARIANT_DD || h->lane_nct >= 0 || (split_it <= 0 && split_tr <= 0) || P.B < 2 || P.order)
-        return launch(h, true, P, st);
+    if (!split_form(h, P.B, split_it, split_tr, 1ll << 62) || P.order) return launch(h, true, P, st);
     unsigned res = 0;
     if (hipError_t e = launch(h, true, P, st, &res)) return e;
-    if ((long long)res * WAVES_PER_BLOCK < P.B) return launch(h, true, P, st);   // the work-queue form
+    const long long slots = (long long)res * WAVES_PER_BLOCK;
+    if (slots < P.B) return launch(h, true, P, st);   // the work-queue form
+    // records for the slots, not for this B: the buffer of a stream never changes size
     const size_t rpl = (size_t)((h->mo4 + WAVE - 1) / WAVE);
-    const size_t rec_bytes = ((size_t)P.B * ckpt_doubles((int)rpl) * sizeof(double) + 255) & ~(size_t)255;
-    const size_t hdr = (size_t)cont_hdr(P.B);
-    const size_t need = rec_bytes + (hdr + (size_t)P.B) * sizeof(uint32_t);
-    void* buf = nullptr;
-    {
-        std::lock_guard<std::mutex> lk(h->split_mtx);
-        Handle::SplitBuf& sb = h->split[st];
-        if (sb.bytes < need) {
-            hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-            if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone)
-                return launch(h, true, P, st);   // no allocation inside a capture: the one-phase form
-            if (sb.p) (void)hipFree(sb.p);
-            sb.p = nullptr;
-            sb.bytes = 0;
-            if (hipError_t e = hipMalloc(&sb.p, need)) return e;
-            sb.bytes = need;
-        }
-        buf = sb.p;
-    }
+    const size_t rec_bytes = ((size_t)slots * ckpt_doubles((int)rpl) * sizeof(double) + 255) & ~(size_t)255;
+    const size_t hdr = (size_t)cont_hdr(slots);
+    const size_t need = rec_bytes + (hdr + (size_t)slots) * sizeof(uint32_t);
+    hipError_t berr = hipSuccess;
+    void* buf = split_buffer(h, st, need, berr);
+    if (berr != hipSuccess) return berr;
+    if (!buf) return launch(h, true, P, st);
     uint32_t* cont = reinterpret_cast<uint32_t*>((char*)buf + rec_bytes);
     if (hipError_t e = hipMemsetAsync(cont, 0, hdr * sizeof(uint32_t), st)) return e;
     const int team = split_tr > 0 ? (int)std::min<long long>(P.B, TEAM_CAP) : 0;
@@ -5803,8 +5843,7 @@ int alipmpc_solve_launches(void* handle, int64_t B, int32_t* launches, int32_t* 
     int64_t slots = 0;
     if (int rc = alipmpc_solve_slots(handle, &slots)) return rc;
     // launch_solve's conditions for the split form (no order / active mask on the batch API)
-    const bool split = h->cfg.variant != ALIPMPC_VARIANT_DD && h->lane_nct < 0 && h->split_it > 0 && B >= 2 &&
-                       B <= slots;
+    const bool split = split_form(h, B, h->split_it, h->split_tr, slots);
     *launches = split ? 2 : 1;
     *team = split && h->split_tr > 0 && h->cfg.precision != ALIPMPC_PREC_FP32 ? 4 : 1;
     return ALIPMPC_OK;

@@ -374,7 +374,8 @@ static void gradient(const oprob* P, const double* u, double* g)
         double rho2 = dxg * dxg + dyg * dyg;
         double phi = X[k][4] - atan2(dyg, dxg);
         for (int j = 0; j < n; ++j) {
-            double dtar = (dxg * (-K->Phi[k][1][j]) - dyg * (-K->Phi[k][0][j])) / rho2;
+            /* (p = goal exactly: the target heading's derivatives are 0 instead of 0 / 0) */
+            double dtar = rho2 > 0.0 ? (dxg * (-K->Phi[k][1][j]) - dyg * (-K->Phi[k][0][j])) / rho2 : 0.0;
             g[j] += 2 * w * (ex * K->Phi[k][0][j] + ey * K->Phi[k][1][j]) + 2 * c->r * phi * (K->Phi[k][4][j] - dtar);
         }
     }
@@ -471,12 +472,13 @@ static void hessian(const oprob* P, const double* u, const double* y, double* H 
         double dxg = P->goal[0] - X[k][0], dyg = P->goal[1] - X[k][1];
         double rho2 = dxg * dxg + dyg * dyg;
         double phi = X[k][4] - atan2(dyg, dxg);
-        double gp[3] = {-dyg / rho2, dxg / rho2, 1.0};
+        double gp[3] = {rho2 > 0.0 ? -dyg / rho2 : 0.0, rho2 > 0.0 ? dxg / rho2 : 0.0, 1.0};   /* (§2 item 7) */
         int idx[3] = {0, 1, 4};
         for (int a = 0; a < 3; ++a)
             for (int b = 0; b < 3; ++b) Hl[k][idx[a]][idx[b]] += 2 * c->r * gp[a] * gp[b];
         double r4 = rho2 * rho2;
-        double h00 = 2 * dxg * dyg / r4, h01 = (dyg * dyg - dxg * dxg) / r4, h11 = -2 * dxg * dyg / r4;
+        double h00 = rho2 > 0.0 ? 2 * dxg * dyg / r4 : 0.0, h01 = rho2 > 0.0 ? (dyg * dyg - dxg * dxg) / r4 : 0.0,
+               h11 = rho2 > 0.0 ? -2 * dxg * dyg / r4 : 0.0;
         Hl[k][0][0] += 2 * c->r * phi * (-h00);
         Hl[k][0][1] += 2 * c->r * phi * (-h01);
         Hl[k][1][0] += 2 * c->r * phi * (-h01);
@@ -741,7 +743,7 @@ static void dd_gradient(const oprob* P, const double* u, double* g)
         double rho2 = dxg * dxg + dyg * dyg, phi = X[k][2] - atan2(dyg, dxg);
         for (int a = 0; a < n; ++a)
             g[a] += 2 * w * (-dxg * Jp[k][0][a] - dyg * Jp[k][1][a]) +
-                    2 * c->r * phi * (Jp[k][2][a] - (dyg * Jp[k][0][a] - dxg * Jp[k][1][a]) / rho2);
+                    2 * c->r * phi * (Jp[k][2][a] - (rho2 > 0.0 ? (dyg * Jp[k][0][a] - dxg * Jp[k][1][a]) / rho2 : 0.0));
     }
     double up0 = P->last_u[0], up1 = P->last_u[1];
     for (int i = 0; i < P->N; ++i) {
@@ -830,12 +832,13 @@ static void dd_hessian(const oprob* P, const double* u, const double* y, double*
         double w = c->q + (k == 1 ? c->p : 0.0);
         double dxg = P->goal[0] - X[k][0], dyg = P->goal[1] - X[k][1];
         double rho2 = dxg * dxg + dyg * dyg, phi = X[k][2] - atan2(dyg, dxg), r4 = rho2 * rho2;
-        double gp[3] = {-dyg / rho2, dxg / rho2, 1.0};
+        double gp[3] = {rho2 > 0.0 ? -dyg / rho2 : 0.0, rho2 > 0.0 ? dxg / rho2 : 0.0, 1.0};   /* (§2 item 7) */
         for (int a = 0; a < 3; ++a)
             for (int b = 0; b < 3; ++b) Hl[k][a][b] += 2 * c->r * gp[a] * gp[b];
         Hl[k][0][0] += 2 * w;
         Hl[k][1][1] += 2 * w;
-        double s00 = 2 * dxg * dyg / r4, s01 = (dyg * dyg - dxg * dxg) / r4, s11 = -2 * dxg * dyg / r4;
+        double s00 = rho2 > 0.0 ? 2 * dxg * dyg / r4 : 0.0, s01 = rho2 > 0.0 ? (dyg * dyg - dxg * dxg) / r4 : 0.0,
+               s11 = rho2 > 0.0 ? -2 * dxg * dyg / r4 : 0.0;
         Hl[k][0][0] -= 2 * c->r * phi * s00;
         Hl[k][0][1] -= 2 * c->r * phi * s01;
         Hl[k][1][0] -= 2 * c->r * phi * s01;

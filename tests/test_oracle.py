@@ -359,3 +359,27 @@ def test_closed_loop_oracle_semantics(coracle, variant):
     for b in np.nonzero(reached)[0]:
         k = r["steps_to_goal"][b]
         assert (r["status"][b, k:] == -10).all() and (r["status"][b, :k] != -10).all()
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+def test_goal_singularity_guard(golden, coracle, variant):
+    """where a planned state sits exactly on the goal, the target heading atan2(g - p) has
+    0 / 0 derivatives (the reference's cal_dtar_ang_du, MPC_LIP_modi.py:650-655, returns NaN there); every
+    implementation takes them as 0 — numpy and C oracles agree, gradient and Hessian finite — and a solve warm-started
+    at such a plan proceeds (the r3 fp32 closed loop had stayed at Error_In_Step_Computation there).  Away from the
+    goal nothing changes (the g1 goldens above)."""
+    g = golden("g1_callbacks_modi")
+    cfg = O.default_cfg(variant, select_obs=0, detour=0)
+    x0, goal = g["x0"][0].copy(), np.array([10.0, 10.0])
+    u = np.tile(x0, 3)
+    u[10:12] = goal                                   # x_3 = u_3 (positions) exactly on the goal
+    pr = O.Problem(cfg, x0, goal, 1, np.zeros((0, 3)), np.zeros((0, 5)))
+    gr = pr.gradient(u)
+    assert np.isfinite(gr).all() and np.isfinite(pr.hessian(u, np.zeros(pr.m))).all()
+    cc = coracle.default_cfg(variant, 3, nc_max=0, ne_max=0, select_obs=0, detour=0)
+    o = coracle.eval_batch(cc, x0[None], goal[None], np.ones(1), np.zeros((1, 0, 3)), np.zeros(1, np.int32), None,
+                           None, u[None])
+    assert rel(o["grad"][0], gr) < REL
+    r = coracle.solve_batch(cc, x0[None], goal[None], np.ones(1, np.int8), np.zeros((1, 0, 3)), np.zeros(1, np.int32),
+                            None, None, u[None])
+    assert r["status"][0] != -3 and np.isfinite(r["u"]).all()

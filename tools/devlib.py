@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""Dev builds for A/B timing (CPU, here): a library whose horizon-N part (solve / eval kernels of one N) comes from a
+variant source and/or extra -D flags, linked with the other parts compiled once from the checked-in source (cached
+under devlib/cache by source hash).  The variant must keep the KP struct and the host ABI unchanged.
+
+  python tools/devlib.py NAME [--src csrc/variant.hip] [--part 3] [-D FLAG ...] [--only-ksm 10]
+  -> devlib/libalipmpc_NAME.so   (load with ALIPMPC_LIB=devlib/libalipmpc_NAME.so; tools/ab_solve.py, tools/ab.sh)
+
+--only-ksm K instantiates the wave program at one row-step count only (ALIP_DEV_ONLY_KSM; cfg2 is K = 10): the part
+compiles ~3x faster, and shapes needing another K are not served by that build.
+"""
+import argparse
+import hashlib
+import os
+import shutil
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "mujoco-lip-mpc-simulation_amd"))
+from alipmpc import build as B  # noqa: E402
+
+OUT = os.path.join(ROOT, "devlib")
+CACHE = os.path.join(OUT, "cache")
+
+
+def _hash(paths, extra):
+    h = hashlib.sha256()
+    for p in paths:
+        with open(p, "rb") as fh:
+            h.update(fh.read())
+    h.update(" ".join(extra).encode())
+    return h.hexdigest()[:16]
+
+
+def part_obj(k, src, extra):
+    os.makedirs(CACHE, exist_ok=True)
+    key = _hash([src, B.INC, B.MATH, B.HDR], [*B.ARCH, *B.FLAGS, *extra, str(k)])
+    o = os.path.join(CACHE, f"part{k}_{key}.o")
+    if not os.path.exists(o):
+        cmd = [B.HIPCC, *B.ARCH, *B.FLAGS, *extra, f"-DALIP_PART={k}", "-c", "-o", o + ".tmp", src]
+        subprocess.check_call(cmd)
+        os.replace(o + ".tmp", o)
+    return o
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("name")
+    ap.add_argument("--src", default=None)
+    ap.add_argument("--part", type=int, default=3)
+    ap.add_argument("-D", dest="defs", action="append", default=[])
+    ap.add_argument("--only-ksm", type=int, default=0)
+    ap.add_argument("--base", default=None, help="source of the other parts (default: csrc/_base_variant.hip if present, "
+                                                 "so editing alipmpc.hip does not recompile them)")
+    a = ap.parse_args()
+    src = os.path.abspath(a.src) if a.src else B.SRC
+    bv = os.path.join(os.path.dirname(B.SRC), "_base_variant.hip")
+    base = os.path.abspath(a.base) if a.base else (bv if os.path.exists(bv) else B.SRC)
+    vx = [f"-D{d}" for d in a.defs] + ([f"-DALIP_DEV_ONLY_KSM={a.only_ksm}"] if a.only_ksm else [])
+    bid = ['-DALIP_BUILD_ID="dev-' + a.name + '"']
+    jobs = []
+    with ThreadPoolExecutor(9) as ex:
+        for k in B.PARTS:
+            if k == a.part:
+                jobs.append(ex.submit(part_obj, k, src, vx + bid))
+            else:
+                jobs.append(ex.submit(part_obj, k, base, ['-DALIP_BUILD_ID="dev"']))
+        objs = [j.result() for j in jobs]
+    os.makedirs(OUT, exist_ok=True)
+    lib = os.path.join(OUT, f"libalipmpc_{a.name}.so")
+    subprocess.check_call([B.HIPCC, *B.ARCH, "-shared", "-fPIC", "-o", lib + ".tmp", *objs])
+    os.replace(lib + ".tmp", lib)
+    print(lib, flush=True)
+
+
+if __name__ == "__main__":
+    main()
