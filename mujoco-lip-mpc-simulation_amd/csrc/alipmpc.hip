@@ -128,6 +128,12 @@ constexpr int SPLIT_IT_DEFAULT = ALIP_SPLIT_IT;   // phase-1 iteration cap of th
 constexpr int SPLIT_TR_DEFAULT = 0;               // phase-1 trial cut of a cold solve (0 = off: no team records)
 constexpr int CL_SPLIT_IT_DEFAULT = 16;           // the closed loop's per-tick solves: phase-1 cap
 constexpr int CL_SPLIT_TR_DEFAULT = 40;           // and trial cut
+constexpr int CL_GROUPS_DEFAULT = 2;              // closed loop: episode groups on streams of their own (4: host-bound)
+static int env_groups()
+{
+    const char* t = std::getenv("ALIPMPC_CL_GROUPS");
+    return t ? std::max(1, std::atoi(t)) : CL_GROUPS_DEFAULT;
+}
 // split-launch counters (KP.cont): single records, team records, then the B instance ids of records (index k)
 constexpr int CONT_SINGLE = 0, CONT_TEAM = 1;
 __host__ __device__ constexpr long long cont_hdr(long long) { return 2; }
@@ -3922,6 +3928,7 @@ __global__ __launch_bounds__(256) void rollout_init_kernel(long long B, int S, i
 // ------------------------------------------------------------------------------------------------
 struct CLP {
     long long B;
+    long long b0;     // global index of episode 0 of this launch (an episode group's offset: the kick's seed index)
     int S, f, s, i, variant, N;
     double ch_r, shb_r, bsh_r, tr;   // ALIP flow over rest_t: cosh, sinh / beta, beta sinh, rest_t / T
     double ch_d, shb_d, bsh_d, td;   // ... over dt = T / f_cyc
@@ -4158,8 +4165,8 @@ __global__ __launch_bounds__(256) void cl_update_kernel(CLP C)
     xn[3] = C.bsh_d * x[1] + C.ch_d * x[3] - C.bsh_d * fy;
     xn[4] = x[4] + C.td * hv[1];
     if (C.kick > 0) {
-        xn[2] += C.kick * (2.0 * cl_uniform(C.seed, b, C.s, C.i, 0) - 1.0);
-        xn[3] += C.kick * (2.0 * cl_uniform(C.seed, b, C.s, C.i, 1) - 1.0);
+        xn[2] += C.kick * (2.0 * cl_uniform(C.seed, C.b0 + b, C.s, C.i, 0) - 1.0);
+        xn[3] += C.kick * (2.0 * cl_uniform(C.seed, C.b0 + b, C.s, C.i, 1) - 1.0);
     }
     for (int c = 0; c < 5; ++c) x[c] = xn[c];
     if (C.i == C.f - 1) {
@@ -4589,6 +4596,10 @@ struct Handle {
     void* rstage = nullptr;
     size_t rstage_bytes = 0;
     hipStream_t own = nullptr;
+    // closed loop: episode groups on streams of their own (ALIPMPC_CL_GROUPS), fork / join events
+    static constexpr int MAXG = 8;
+    hipStream_t gst[MAXG] = {};
+    hipEvent_t gev[MAXG + 1] = {};
     // split launch of the wave program (ALIPMPC_SPLIT_IT): the phase-1 iteration cap (0 = off) and, per stream, the
     // record buffer (launches on one stream run in order, so they may share it; other streams get their own)
     int split_it = 0;
@@ -5597,39 +5608,100 @@ int alipmpc_closed_loop_batch(void* handle, int64_t B, int32_t S, int32_t f_cyc,
     // search halves ~20 times per iteration (tools/cl_wstamps.py, profiles/r3/wst): 52.13 vs 52.00 ms per loop
     const char* oe = std::getenv("ALIPMPC_CL_ORDER");
     const bool order_ok = cf.program != ALIPMPC_PROGRAM_LANE && oe && std::strcmp(oe, "1") == 0;
+    // Episode groups (ALIPMPC_CL_GROUPS, >= 256 episodes each): contiguous ranges of episodes whose ticks run on
+    // streams of their own, so a tick that waits on one slow instance holds back only its group; the other groups'
+    // launches fill the device meanwhile.  Every episode runs the same kernels on the same values (the kick is seeded
+    // by the global episode index), so the outputs do not depend on the grouping (GPU test).
+    int G = env_groups();
+#ifdef ALIP_WSTAMP
+    G = 1;   // (diagnostic records are indexed by the whole batch)
+#endif
+    if (order_ok) G = 1;   // (the opt-in launch order is a permutation of the whole batch)
+    G = (int)std::max<long long>(1, std::min<long long>({(long long)G, (long long)Handle::MAXG, B / 256}));
+    struct Grp {
+        CLP C;
+        KP P;
+        hipStream_t s;
+        unsigned g1;
+    } grp[Handle::MAXG];
+    const long long nn = n, SF = (long long)S * f_cyc;
+    for (int g = 0; g < G; ++g) {
+        const long long b0 = B * g / G, Bg = B * (g + 1) / G - b0;
+        auto o = [&](auto& p, long long per) {
+            if (p) p += b0 * per;
+        };
+        CLP c = C;
+        c.B = Bg;
+        c.b0 = b0;
+        o(c.goal, 2); o(c.x, 5); o(c.pst, 2); o(c.hdv, 4); o(c.mhd, 3); o(c.plan, nn); o(c.leg, 1); o(c.flags, 1);
+        o(c.xs, 5); o(c.u0, nn); o(c.sleg, 1); o(c.u, nn); o(c.foot, 3); o(c.x_pred, nn); o(c.status, 1);
+        o(c.iters, 1); o(c.active, 1); o(c.foot_traj, 3LL * S); o(c.x_traj, 5LL * (S + 1)); o(c.hd_traj, 2LL * S);
+        o(c.status_traj, SF); o(c.iters_traj, SF); o(c.steps_to_goal, 1); o(c.action_traj, 8 * SF); o(c.vdes, 2);
+        o(c.pose0, 3);
+        KP q = P;
+        q.B = Bg;
+        o(q.goal, 2); o(q.cir, 3LL * cf.nc_max); o(q.nc, 1); o(q.elp, 5LL * cf.ne_max); o(q.ne, 1); o(q.x0, 5);
+        o(q.leg, 1); o(q.u0, nn); o(q.active, 1); o(q.u_out, nn); o(q.foot_out, 3); o(q.x_pred, nn); o(q.status, 1);
+        o(q.iters, 1);
+        grp[g].C = c;
+        grp[g].P = q;
+        grp[g].g1 = (unsigned)((Bg + 255) / 256);
+        grp[g].s = st;
+        if (G > 1) {
+            if (!h->gst[g]) HIPCHK(h, hipStreamCreateWithFlags(&h->gst[g], hipStreamNonBlocking));
+            if (!h->gev[g]) HIPCHK(h, hipEventCreateWithFlags(&h->gev[g], hipEventDisableTiming));
+            grp[g].s = h->gst[g];
+        }
+    }
+    if (G > 1 && !h->gev[Handle::MAXG]) HIPCHK(h, hipEventCreateWithFlags(&h->gev[Handle::MAXG], hipEventDisableTiming));
     const int ei = h->evi;
     h->evi = (ei + 1) % Handle::NEV;
     HIPCHK(h, hipEventRecord(h->ev[ei][0], st));
+    if (G > 1) {   // fork
+        HIPCHK(h, hipEventRecord(h->gev[Handle::MAXG], st));
+        for (int g = 0; g < G; ++g) HIPCHK(h, hipStreamWaitEvent(grp[g].s, h->gev[Handle::MAXG], 0));
+    }
     for (int s = 0; s < S; ++s) {
         for (int i = 0; i < f_cyc; ++i) {
             // rest_t = step_t - i * (step_t / f_cyc)   (main_sim_mpc.py:78)
             const double rest = T - i * (T / f_cyc);
-            C.s = s;
-            C.i = i;
-            C.ch_r = std::cosh(beta * rest); C.shb_r = std::sinh(beta * rest) / beta;
-            C.bsh_r = std::sinh(beta * rest) * beta; C.tr = rest * (1.0 / T);
-            hipLaunchKernelGGL(cl_project_kernel, dim3(g1), dim3(256), 0, st, C);
-            HIPCHK(h, hipGetLastError());
-            // wave program: after the first tick, solve last tick's long instances first (same bits per instance)
-            P.order = nullptr;
-            if (order_ok && (s > 0 || i > 0)) {
-                hipLaunchKernelGGL(cl_order_kernel, dim3(1), dim3(CL_ORDER_THREADS), 0, st, (const int32_t*)l.it,
-                                   (const uint8_t*)l.act, (long long)B, l.ord);
+            for (int g = 0; g < G; ++g) {
+                CLP& Cg = grp[g].C;
+                KP& Pg = grp[g].P;
+                const hipStream_t sg = grp[g].s;
+                Cg.s = s;
+                Cg.i = i;
+                Cg.ch_r = std::cosh(beta * rest); Cg.shb_r = std::sinh(beta * rest) / beta;
+                Cg.bsh_r = std::sinh(beta * rest) * beta; Cg.tr = rest * (1.0 / T);
+                hipLaunchKernelGGL(cl_project_kernel, dim3(grp[g].g1), dim3(256), 0, sg, Cg);
                 HIPCHK(h, hipGetLastError());
-                P.order = l.ord;
-            }
-            P.queue = h->dq + 2 * (h->qi.fetch_add(1u) % Handle::NQ);
+                // wave program: after the first tick, solve last tick's long instances first (same bits per instance)
+                Pg.order = nullptr;
+                if (order_ok && (s > 0 || i > 0)) {
+                    hipLaunchKernelGGL(cl_order_kernel, dim3(1), dim3(CL_ORDER_THREADS), 0, sg, (const int32_t*)l.it,
+                                       (const uint8_t*)l.act, (long long)B, l.ord);
+                    HIPCHK(h, hipGetLastError());
+                    Pg.order = l.ord;
+                }
+                Pg.queue = h->dq + 2 * (h->qi.fetch_add(1u) % Handle::NQ);
 #ifdef ALIP_WSTAMP
-            {   // diagnostic record slots of this tick: (s f_cyc + i) B + instance
-                const long long base = ((long long)s * f_cyc + i) * B;
-                HIPCHK(h, hipMemcpyToSymbolAsync(HIP_SYMBOL(alip::g_wstamp_base), &base, sizeof(base), 0,
-                                                 hipMemcpyHostToDevice, st));
-                HIPCHK(h, hipStreamSynchronize(st));   // &base is a stack value
-            }
+                {   // diagnostic record slots of this tick: (s f_cyc + i) B + instance
+                    const long long base = ((long long)s * f_cyc + i) * B;
+                    HIPCHK(h, hipMemcpyToSymbolAsync(HIP_SYMBOL(alip::g_wstamp_base), &base, sizeof(base), 0,
+                                                     hipMemcpyHostToDevice, sg));
+                    HIPCHK(h, hipStreamSynchronize(sg));   // &base is a stack value
+                }
 #endif
-            HIPCHK(h, launch_solve(h, P, st, h->cl_split_it, h->cl_split_tr));
-            hipLaunchKernelGGL(cl_update_kernel, dim3(g1), dim3(256), 0, st, C);
-            HIPCHK(h, hipGetLastError());
+                HIPCHK(h, launch_solve(h, Pg, sg, h->cl_split_it, h->cl_split_tr));
+                hipLaunchKernelGGL(cl_update_kernel, dim3(grp[g].g1), dim3(256), 0, sg, Cg);
+                HIPCHK(h, hipGetLastError());
+            }
+        }
+    }
+    if (G > 1) {   // join
+        for (int g = 0; g < G; ++g) {
+            HIPCHK(h, hipEventRecord(h->gev[g], grp[g].s));
+            HIPCHK(h, hipStreamWaitEvent(st, h->gev[g], 0));
         }
     }
     HIPCHK(h, hipEventRecord(h->ev[ei][1], st));
@@ -5887,6 +5959,11 @@ void alipmpc_destroy(void* handle)
         for (hipEvent_t e : pr)
             if (e) hipEventDestroy(e);
     if (h->own) hipStreamDestroy(h->own);
+    for (int g = 0; g < Handle::MAXG; ++g) {
+        if (h->gst[g]) hipStreamDestroy(h->gst[g]);
+        if (h->gev[g]) hipEventDestroy(h->gev[g]);
+    }
+    if (h->gev[Handle::MAXG]) hipEventDestroy(h->gev[Handle::MAXG]);
     delete h;
 }
 

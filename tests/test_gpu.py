@@ -1348,8 +1348,8 @@ def test_split_launch_graph_capture_keeps_its_records(gpu_lib):
 def test_closed_loop_split_team_bit_identical(gpu_lib, variant, kick, B, prec, monkeypatch):
     """The closed loop's per-tick solves run as split launches (ALIPMPC_CL_SPLIT_IT: phase-1 cap, then the
     unfinished instances resume from their records; ALIPMPC_CL_SPLIT_TR: an instance at that many line-search trials
-    is cut early and resumes as a team of 4 waves that evaluates consecutive trials in one round).  Stopped episodes are skipped in phase 1 and never recorded.  Every
-    output equals the one-phase loop's (ALIPMPC_CL_SPLIT_IT=0) bit for bit."""
+    is cut early and resumes as a team of 4 waves that evaluates consecutive trials in one round), with the episodes
+    in groups on streams of their own or not.  Every output equals the one-phase, one-group loop's bit for bit."""
     from alipmpc import scenes
     S, F = 2, 40
     bt = scenes.make_batch(B, seed=710 + variant + 3 * prec, n_cir=5)
@@ -1363,12 +1363,15 @@ def test_closed_loop_split_team_bit_identical(gpu_lib, variant, kick, B, prec, m
     s0 = gpu_lib.Solver(cfg)
     foot0 = s0.solve(x0, bt["goal"], leg, bt["cir"], bt["nc"], u0=np.tile(x0, (1, 3)))["foot"][:, 0:2]
     outs = {}
-    for cut, tr in (("0", "0"), ("16", "40"), ("3", "0"), ("8", "5")):
+    # (ALIPMPC_CL_GROUPS: contiguous episode groups whose ticks run on streams of their own)
+    for cut, tr, grp in (("0", "0", "1"), ("16", "40", "4"), ("3", "0", "3"), ("8", "5", "1"), ("0", "0", "4")):
         monkeypatch.setenv("ALIPMPC_CL_SPLIT_IT", cut)
         monkeypatch.setenv("ALIPMPC_CL_SPLIT_TR", tr)
-        outs[cut + "/" + tr] = gpu_lib.Solver(cfg).closed_loop(x0, foot0, bt["goal"], leg, bt["cir"], bt["nc"],
-                                                               steps=S, f_cyc=F, kick=kick, seed=3)
-    ref = outs.pop("0/0")
+        monkeypatch.setenv("ALIPMPC_CL_GROUPS", grp)
+        outs[cut + "/" + tr + "/" + grp] = gpu_lib.Solver(cfg).closed_loop(x0, foot0, bt["goal"], leg, bt["cir"],
+                                                                           bt["nc"], steps=S, f_cyc=F, kick=kick,
+                                                                           seed=3)
+    ref = outs.pop("0/0/1")
     assert (ref["status"] == 2).sum() > 0 and (ref["steps_to_goal"] > 0).sum() > 0
     for name, o in outs.items():
         for k in ref:

@@ -1,4 +1,4 @@
-"""Dev (for the episode-group build, commit 429e42c): closed-loop outputs with the episodes in groups on streams of their own (ALIPMPC_CL_GROUPS) vs one group, on a
+"""Dev: closed-loop outputs with the episodes in groups on streams of their own (ALIPMPC_CL_GROUPS) vs one group, on a
 batch with stops, kicks and infeasible scenes (bit identity), under ALIPMPC_LIB.  python tools/groups_check.py"""
 import os
 import sys

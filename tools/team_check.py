@@ -18,8 +18,8 @@ leg = bt["leg"].astype(np.int8)
 cfg = alipmpc.default_cfg(0, 3, nc_max=5, ne_max=0)
 foot0 = alipmpc.Solver(cfg).solve(x0, bt["goal"], leg, bt["cir"], bt["nc"], u0=np.tile(x0, (1, 3)))["foot"][:, 0:2]
 ref = None
-for cut, tr in (("0", "0"), ("16", "0"), ("0", "40"), ("16", "40"), ("0", "1000"), ("0", "12"), ("8", "5"), ("0", "0")):
-    os.environ["ALIPMPC_CL_SPLIT_IT"], os.environ["ALIPMPC_CL_SPLIT_TR"] = cut, tr
+for cut, tr, grp in (("0", "0", "1"), ("16", "40", "1"), ("0", "0", "4"), ("16", "40", "4"), ("16", "40", "2"), ("0", "12", "8")):
+    os.environ["ALIPMPC_CL_SPLIT_IT"], os.environ["ALIPMPC_CL_SPLIT_TR"], os.environ["ALIPMPC_CL_GROUPS"] = cut, tr, grp
     o = alipmpc.Solver(cfg).closed_loop(x0, foot0, bt["goal"], leg, bt["cir"], bt["nc"], steps=S, f_cyc=F, seed=3)
     if ref is None:
         ref = o
@@ -29,4 +29,4 @@ for cut, tr in (("0", "0"), ("16", "0"), ("0", "40"), ("16", "40"), ("0", "1000"
     if bad["foot"]:
         d = (o["foot"] != ref["foot"]).reshape(B, -1).any(axis=1)
         first = int(np.argmax(d))
-    print(f"cut {cut} tr {tr}: episodes differing per output {bad} first {first}", flush=True)
+    print(f"cut {cut} tr {tr} groups {grp}: episodes differing per output {bad} first {first}", flush=True)
