@@ -226,6 +226,9 @@ def main():
     # converged and how many returned plans are feasible for the reference constraints
     feas = feasible_fraction(alipmpc, solver, cfg, inp, out, dev, world, dist)
 
+    # the wave program's binding resource is the per-iteration dependency chain of its slowest instances (MFMA busy
+    # ~0.05, VALU issue ~0.5): the critical instance's iteration time alone on its SIMD, live, against the issue floor
+    lat = latency_probe(solver, inp, out, iters, prof, dev) if (rank == 0 and program == "wave") else None
     sweep = jacobian_sweep(alipmpc, scenes, variant, args, dev) if (rank == 0 and args.sweep_batch > 0) else None
     cl = closed_loop_rate(solver, inp, out, args.closed_loop_steps, dev) \
         if (rank == 0 and args.closed_loop_steps > 0) else None
@@ -276,7 +279,11 @@ def main():
             },
             "roofline": {
                 "kernel": kname,
-                "bound": "mfma" if program == "wave" else "valu",
+                # wave program: a latency chain (MFMA busy ~0.05 of the SIMD cycles), see "latency"; lane program: vector
+                # issue of the fp64 KKT algebra
+                "bound": ("latency" if (prof.get("mfma_busy_share") is None or prof["mfma_busy_share"] < 0.1) else "mfma")
+                if program == "wave" else "valu",
+                "latency": lat,
                 "achieved": achieved,
                 "peak": peak,
                 "unit": "TFLOP/s",
@@ -379,6 +386,35 @@ def counter_record(key, bid):
     except (OSError, ValueError):
         return {}
     return rec if rec.get("build_id") == bid else {}
+
+
+CLOCK_GHZ = 2.4   # MI355X max engine clock (MI355X_MICROARCH.md); cycle figures below are at this clock
+ISSUE_CYC = 4     # one wave alone issues at most one instruction per 4 cycles (MI355X_MICROARCH.md: s_nop / v_fma 4)
+
+
+def latency_probe(solver, inp, out, iters, prof, dev, copies=64, reps=5):
+    """The critical instance's interior-point iteration time with its SIMD to itself: the batch's instance with the
+    most iterations, solved as `copies` identical instances (one wave each, one per SIMD), mean launch time over reps
+    launches / its iterations -> cycles per iteration at CLOCK_GHZ.  Against the instruction-issue floor of one wave
+    (insts_per_iter x ISSUE_CYC, from the build's committed counter record): frac = floor / measured."""
+    import torch
+    b = int(np.argmax(iters))
+    sub = {k: v[b:b + 1].repeat((copies,) + (1,) * (v.dim() - 1)).contiguous() for k, v in inp.items()}
+    o = {k: torch.empty((copies,) + tuple(v.shape[1:]), dtype=v.dtype, device=dev) for k, v in out.items()}
+    st = torch.cuda.current_stream(dev)
+    ms = []
+    for r in range(reps + 2):
+        solver.solve_device(sub, o, stream=st)
+        torch.cuda.synchronize(dev)
+        if r >= 2:
+            ms.append(solver.last_kernel_ms())
+    it = int(o["iters"][0].item())
+    cyc = float(np.mean(ms)) * 1e-3 * CLOCK_GHZ * 1e9 / max(it, 1)
+    ipi = prof.get("insts_per_iter")
+    floor = ipi * ISSUE_CYC if ipi else None
+    return {"instance_iters": it, "launch_ms": float(np.mean(ms)), "cycles_per_iter": cyc, "clock_ghz": CLOCK_GHZ,
+            "issue_floor_cycles": floor, "frac": (floor / cyc) if floor else None,
+            "note": "critical instance alone on its SIMD; floor = counter insts_per_iter x 4 cycles (one wave's issue)"}
 
 
 def jacobian_sweep(alipmpc, scenes, variant, args, dev, reps=20):

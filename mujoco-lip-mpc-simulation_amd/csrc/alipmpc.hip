@@ -605,8 +605,44 @@ __device__ __forceinline__ double row_eval(const KP& P, const RowInfo& ri, const
 // Computed in fp64 for either workspace type (the discrete select/detour decisions do not depend on
 // cfg.precision); results are stored into the workspace's type.
 // ------------------------------------------------------------------------------------------------
+// 1/sqrt(d) and 1/x to ~1 ulp: hardware estimate + two Newton steps (a few FMAs instead of the
+// ~15-instruction IEEE sqrt / div sequences on the Cholesky critical path)
+// binary exponent of a normal nonzero value (the trial count of a line search from a = ap 2^-j)
+__device__ __forceinline__ int fexp2(double x) { return __builtin_amdgcn_frexp_exp(x); }
+__device__ __forceinline__ int fexp2(float x) { return __builtin_amdgcn_frexp_expf(x); }
+
+__device__ __forceinline__ double rsqrt_nr(double d)
+{
+    double y = __builtin_amdgcn_rsq(d);
+    const double h = 0.5 * d;
+    y = y * fma(-h * y, y, 1.5);
+    y = y * fma(-h * y, y, 1.5);
+    return y;
+}
+__device__ __forceinline__ double rcp_nr(double x)
+{
+    double y = __builtin_amdgcn_rcp(x);
+    double e = fma(-x, y, 1.0);
+    y = fma(y, e, y);
+    e = fma(-x, y, 1.0);
+    return fma(y, e, y);
+}
+// fp32: the hardware estimates are ~1 ulp already; one Newton step makes them correctly rounded-ish
+__device__ __forceinline__ float rsqrt_nr(float d)
+{
+    float y = __builtin_amdgcn_rsqf(d);
+    return y * fmaf(-0.5f * d * y, y, 1.5f);
+}
+__device__ __forceinline__ float rcp_nr(float x)
+{
+    float y = __builtin_amdgcn_rcpf(x);
+    return fmaf(y, fmaf(-x, y, 1.0f), y);
+}
+
+#include "fastmath.inc"
+
 template <int N, class WT>
-__device__ void prologue(const KP& P, const WT& w, const typename WT::real* G, const typename WT::real* E,
+__device__ void prologue(const KP& P, const WT& w, const typename WT::real* G, const double* E,
                          long long b, double& gxg, double& gyg, int& legv, double& uj)
 {
     using D = Dim<N>;
@@ -673,11 +709,11 @@ __device__ void prologue(const KP& P, const WT& w, const typename WT::real* G, c
         double nx = 0, ny = 0;
         if (lane < ncs) {
             const auto* c = w.obs + 3 * lane;
-            double cen = (x0v0 - c[0]) * (x0v0 - c[0]) + (x0v1 - c[1]) * (x0v1 - c[1]);
-            double gd = (x0v0 - g0) * (x0v0 - g0) + (x0v1 - g1) * (x0v1 - g1);
+            double cen = fma(x0v0 - c[0], x0v0 - c[0], (x0v1 - c[1]) * (x0v1 - c[1]));
+            double gd = fma(x0v0 - g0, x0v0 - g0, (x0v1 - g1) * (x0v1 - g1));
             if (cen < gd && cen < 9 * c[2] * c[2]) {
-                double th = atan2(g1 - x0v1, g0 - x0v0);
-                double al = atan2(c[1] - x0v1, c[0] - x0v0);
+                double th = latan2(g1 - x0v1, g0 - x0v0);   // (the lane program's and the eval hook's functions)
+                double al = latan2(c[1] - x0v1, c[0] - x0v0);
                 double dd = th - al;
                 if (dd < 0 && fabs(dd) > M_PI)
                     dd += 2 * M_PI;
@@ -688,9 +724,9 @@ __device__ void prologue(const KP& P, const WT& w, const typename WT::real* G, c
                     double na = dd < 0 ? th - M_PI / 12 : th + M_PI / 12;
                     double rr = sqrt(gd);
                     double sn, cs;
-                    sincos(na, &sn, &cs);
-                    nx = x0v0 + rr * cs;
-                    ny = x0v1 + rr * sn;
+                    lsincos(na, &sn, &cs);
+                    nx = fma(rr, cs, x0v0);   // (explicit fma: every kernel's detour goal rounds alike)
+                    ny = fma(rr, sn, x0v1);
                 }
             }
         }
@@ -735,41 +771,6 @@ __device__ void prologue(const KP& P, const WT& w, const typename WT::real* G, c
     wave_sync();
 }
 
-// 1/sqrt(d) and 1/x to ~1 ulp: hardware estimate + two Newton steps (a few FMAs instead of the
-// ~15-instruction IEEE sqrt / div sequences on the Cholesky critical path)
-// binary exponent of a normal nonzero value (the trial count of a line search from a = ap 2^-j)
-__device__ __forceinline__ int fexp2(double x) { return __builtin_amdgcn_frexp_exp(x); }
-__device__ __forceinline__ int fexp2(float x) { return __builtin_amdgcn_frexp_expf(x); }
-
-__device__ __forceinline__ double rsqrt_nr(double d)
-{
-    double y = __builtin_amdgcn_rsq(d);
-    const double h = 0.5 * d;
-    y = y * fma(-h * y, y, 1.5);
-    y = y * fma(-h * y, y, 1.5);
-    return y;
-}
-__device__ __forceinline__ double rcp_nr(double x)
-{
-    double y = __builtin_amdgcn_rcp(x);
-    double e = fma(-x, y, 1.0);
-    y = fma(y, e, y);
-    e = fma(-x, y, 1.0);
-    return fma(y, e, y);
-}
-// fp32: the hardware estimates are ~1 ulp already; one Newton step makes them correctly rounded-ish
-__device__ __forceinline__ float rsqrt_nr(float d)
-{
-    float y = __builtin_amdgcn_rsqf(d);
-    return y * fmaf(-0.5f * d * y, y, 1.5f);
-}
-__device__ __forceinline__ float rcp_nr(float x)
-{
-    float y = __builtin_amdgcn_rcpf(x);
-    return fmaf(y, fmaf(-x, y, 1.0f), y);
-}
-
-#include "fastmath.inc"
 
 // ------------------------------------------------------------------------------------------------
 // register Cholesky: lane i (< n) holds row i of the (regularised) KKT matrix in a[0..n-1].
@@ -847,18 +848,22 @@ __device__ __forceinline__ bool gj_lds(R* M, int lane)
 template <int n, class R>
 __device__ __forceinline__ bool gj_regs(R (&a)[n + 1], int lane)
 {
+    // r4: the pivot row is not normalised during the elimination (row i -= (a_ip / a_pp) row p for i != p; row p
+    // stays), so no per-entry select between the pivot row and the others; the diagonal left at the end divides the
+    // right-hand side once per lane.  The pivots a_pp are the same D of K = L D L^T (the positive-definiteness test).
 #pragma unroll
     for (int p = 0; p < n; ++p) {
         const R d = bcast(a[p], p);
         if (!(d > R(0))) return false;   // wave-uniform
-        const R inv = rcp_nr(d);
-        const R f = a[p];
+        const R m = lane == p ? R(0) : a[p] * rcp_nr(d);
 #pragma unroll
-        for (int j = p + 1; j <= n; ++j) {
-            const R pj = bcast(a[j], p) * inv;
-            a[j] = lane == p ? pj : fma(-f, pj, a[j]);
-        }
+        for (int j = p + 1; j <= n; ++j) a[j] = fma(-m, bcast(a[j], p), a[j]);
     }
+    // lane i: x_i = a_i[n] / a_i[i]
+    R dg = a[0];
+#pragma unroll
+    for (int i = 1; i < n; ++i) dg = lane == i ? a[i] : dg;
+    a[n] = a[n] * rcp_nr(dg);
     return true;
 }
 
@@ -1066,7 +1071,7 @@ __device__ __forceinline__ void row_coef(int type, int k, const R (&v)[4], R a0,
     const R w = C.q + (k == 1 ? C.p : R(0));
     const R dxg = C.gxg - v[0], dyg = C.gyg - v[1];
     // (at p = goal exactly the target heading atan2(0, 0) = 0 is taken as locally constant: DESIGN.md §2 item 7)
-    const R rho2 = dxg * dxg + dyg * dyg, ir2 = rho2 > R(0) ? R(1) / rho2 : R(0);
+    const R rho2 = dxg * dxg + dyg * dyg, ir2 = rho2 > R(0) ? rcp_nr(rho2) : R(0);
     const R gp0 = -dyg * ir2, gp1 = dxg * ir2, phi = a0;
     R c0 = R(0), c1 = R(0), c2 = R(0), c3 = R(0);
     if (vel) {
@@ -1187,7 +1192,7 @@ __device__ __forceinline__ R obj_sum(const R (&v)[RPL], int mr4)
 // Without TM all of it compiles out: the interior-point loop of the plain build sits at its register budget, and the
 // team logic in the same body had cost 36 -> 172 B/lane of spills (the register allocator, not the arithmetic).
 template <int N, int KSM, class R, bool Q, bool TM = false>
-__device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int wv, long long b, long long rec = -1,
+__device__ __forceinline__ void solve_one(const KP& P0, R* G, R* wsb, int wv, long long b, long long rec = -1,
                                           int tm = 0)
 {
     if constexpr (!TM) tm = 0;
@@ -1227,7 +1232,7 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
 
     double gxg, gyg, uj;
     int legv;
-    prologue<N>(P, w, G, E, b, gxg, gyg, legv, uj);
+    prologue<N>(P, w, G, P.E, b, gxg, gyg, legv, uj);   // (E from global memory: read once per instance)
     const int nc_sel = w.nsel[0], ne_sel = w.nsel[1];
     // unified quadratic forms per obstacle row slot (zero form for unused slots)
     {
@@ -1338,7 +1343,7 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
         const R dl = sr[q] - cl[q], du = cu[q] - sr[q];
         idl[q] = HL(q) ? R(1.0) / dl : R(0.0);
         idu[q] = HU(q) ? R(1.0) / du : R(0.0);
-        lg0 += HL(q) ? (HU(q) ? llog(dl * du) : llog(dl)) : (HU(q) ? llog(du) : R(0.0));
+        lg0 += llog(HL(q) ? (HU(q) ? dl * du : dl) : (HU(q) ? du : R(1.0)));   // (one log per lane: log 1 = 0)
         if (rtype[q] < R_NONE) th0 += fabs(cr[q] - sr[q]);
     }
     wsum2(th0, nbl);
@@ -1550,14 +1555,16 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
             // (max(ru)/sd == max(ru/sd): division by sd > 0 and its rounding are monotone, so the stationarity
             // and feasibility maxima share one reduction)
             nz = wsum(nz);
-            const R sd = uni(fmax(R(100.0), nz / (w.cst[K_MACT] + n)) / R(100.0));
-            const R sc = uni(fmax(R(100.0), nz / fmax(R(1.0), w.cst[K_NBL])) / R(100.0));
-            const R base_err = wmax(fmax(ru / sd, rcm));
+            // (r4: divisions as rcp_div / div100 — a reciprocal and its residual correction instead of the IEEE
+            // division sequence)
+            const R sd = uni(div100(fmax(R(100.0), rcp_div(nz, w.cst[K_MACT] + n))));
+            const R sc = uni(div100(fmax(R(100.0), rcp_div(nz, fmax(R(1.0), w.cst[K_NBL])))));
+            const R base_err = wmax(fmax(rcp_div(ru, sd), rcm));
             whi = wmax(whi);
             wlo = wmin(wlo);
             const bool anyw = whi >= wlo;
             const R comp0 = anyw ? fmax(fabs(whi), fabs(wlo)) : R(0.0);
-            e0 = uni(fmax(base_err, comp0 / sc));
+            e0 = uni(fmax(base_err, rcp_div(comp0, sc)));
             if (e0 <= w.cst[K_TOL]) {
                 status = 0;
                 break;
@@ -1567,7 +1574,7 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
             const R mu_prev = mu;
             for (int t = 0; t < 8; ++t) {
                 const R cm = anyw ? fmax(fabs(whi - mu), fabs(wlo - mu)) : R(0.0);
-                if (fmax(base_err, cm / sc) <= R(10.0) * mu && mu > mu_min)
+                if (fmax(base_err, rcp_div(cm, sc)) <= R(10.0) * mu && mu > mu_min)
                     mu = uni(fmax(mu_min, fmin(R(0.2) * mu, mu * sqrt(mu))));
                 else
                     break;
@@ -1847,7 +1854,9 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
         } else {
             amin = gth;
         }
-        amin = uni(amin * gal);
+        // floor 2^-60: with theta = 0 exactly the formula gives 0 and the trials a = ap 2^-j
+        // would never fall below it
+        amin = uni(fmax(amin * gal, R(8.673617379884035e-19)));
         STAMP(6);
         // ---- filter line search on trial points V + a dV (row registers only)
         // Trial j is a_j = ap 2^-j (and log a_j by the same sequential subtractions); the search takes the first
@@ -1894,7 +1903,9 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
                     const R d1 = st - cl[q], d2 = cu[q] - st;
                     if (HL(q) && !(d1 > 0)) bad = true;
                     if (HU(q) && !(d2 > 0)) bad = true;
-                    lgt += HL(q) ? (HU(q) ? llog(d1 * d2) : llog(d1)) : (HU(q) ? llog(d2) : R(0.0));
+                    // one log per lane (the bound pattern selects its argument; log 1 = 0): the three-way select of
+                    // logs had compiled to three log evaluations per trial
+                    lgt += llog(HL(q) ? (HU(q) ? d1 * d2 : d1) : (HU(q) ? d2 : R(1.0)));
                 }
                 tht = wsum(tht);
                 ft = obj_sum<N, RPL>(ctr, mr4);
@@ -2028,7 +2039,7 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* E, R* wsb, int 
                     v = fmin(v, cu[q] - pu);
                 sr[q] = rtype[q] < R_NONE ? v : R(0.0);
                 const R d1 = sr[q] - cl[q], d2 = cu[q] - sr[q];
-                lr += HL(q) ? (HU(q) ? llog(d1 * d2) : llog(d1)) : (HU(q) ? llog(d2) : R(0.0));
+                lr += llog(HL(q) ? (HU(q) ? d1 * d2 : d1) : (HU(q) ? d2 : R(1.0)));
 
             }
             lr = wsum(lr);
@@ -2173,11 +2184,10 @@ __global__ __launch_bounds__(256, (solve_waves<KSM, R>())) void solve_kernel(KP 
     extern __shared__ __attribute__((aligned(16))) double smem[];
     KP* Ps = reinterpret_cast<KP*>(smem);
     R* G = reinterpret_cast<R*>(smem + KP_DOUBLES);
-    R* E = G + NG * NCP;
-    R* wsb = E + ((NG * 5 + 3) & ~3);
+    // (r4: no LDS copy of E — the prologue reads it from global memory once per instance)
+    R* wsb = G + NG * NCP;
     if (threadIdx.x == 0) *Ps = Pv;
     for (int i = threadIdx.x; i < NG * NCP; i += blockDim.x) G[i] = Pv.G[i];
-    for (int i = threadIdx.x; i < NG * 5; i += blockDim.x) E[i] = Pv.E[i];
     __syncthreads();
     const KP& P = *Ps;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);   // wave-uniform (SGPR)
@@ -2210,7 +2220,7 @@ __global__ __launch_bounds__(256, (solve_waves<KSM, R>())) void solve_kernel(KP 
         rec = __builtin_amdgcn_readfirstlane((int)rec);
         // (one call site: the team solves run the very machine code of the single ones — two inlined copies had
         // rounded differently)
-        if (b >= 0) solve_one<N, KSM, R, false, TM>(P, G, E, wsb, wv, b, rec, team ? -1 - wv : 0);
+        if (b >= 0) solve_one<N, KSM, R, false, TM>(P, G, wsb, wv, b, rec, team ? -1 - wv : 0);
     } else {
         uint32_t* const q = Pv.queue;
         for (long long k = next_instance(q); k < Pv.B; k = next_instance(q)) {
@@ -2219,7 +2229,7 @@ __global__ __launch_bounds__(256, (solve_waves<KSM, R>())) void solve_kernel(KP 
             // solve_one — fp32 contraction / packing decisions otherwise differ between them)
             long long rec = -1;
             asm volatile("" : "+s"(rec));
-            if (!Pv.active || Pv.active[b]) solve_one<N, KSM, R, true>(P, G, E, wsb, wv, b, rec);   // rollout: skip finished
+            if (!Pv.active || Pv.active[b]) solve_one<N, KSM, R, true>(P, G, wsb, wv, b, rec);   // rollout: skip finished
         }
         queue_exit(q);
     }
@@ -2405,11 +2415,11 @@ __device__ __forceinline__ void eval_group_one(const KP& P, const GWS<N>& w, con
         double nx = 0, ny = 0;
         if (j < ncs) {
             const double* c = w.obs + 3 * j;
-            const double cen = (x0v0 - c[0]) * (x0v0 - c[0]) + (x0v1 - c[1]) * (x0v1 - c[1]);
-            const double gd = (x0v0 - g0) * (x0v0 - g0) + (x0v1 - g1) * (x0v1 - g1);
+            const double cen = fma(x0v0 - c[0], x0v0 - c[0], (x0v1 - c[1]) * (x0v1 - c[1]));
+            const double gd = fma(x0v0 - g0, x0v0 - g0, (x0v1 - g1) * (x0v1 - g1));
             if (cen < gd && cen < 9 * c[2] * c[2]) {
-                const double th = atan2(g1 - x0v1, g0 - x0v0);
-                const double al = atan2(c[1] - x0v1, c[0] - x0v0);
+                const double th = latan2(g1 - x0v1, g0 - x0v0);
+                const double al = latan2(c[1] - x0v1, c[0] - x0v0);
                 double dd = th - al;
                 if (dd < 0 && fabs(dd) > M_PI)
                     dd += 2 * M_PI;
@@ -2420,9 +2430,9 @@ __device__ __forceinline__ void eval_group_one(const KP& P, const GWS<N>& w, con
                     const double na = dd < 0 ? th - M_PI / 12 : th + M_PI / 12;
                     const double rr = sqrt(gd);
                     double sn, cs;
-                    sincos(na, &sn, &cs);
-                    nx = x0v0 + rr * cs;
-                    ny = x0v1 + rr * sn;
+                    lsincos(na, &sn, &cs);
+                    nx = fma(rr, cs, x0v0);   // (explicit fma: every kernel's detour goal rounds alike)
+                    ny = fma(rr, sn, x0v1);
                 }
             }
         }
@@ -2466,8 +2476,10 @@ __device__ __forceinline__ void eval_group_one(const KP& P, const GWS<N>& w, con
         fk = wk * (ex * ex + ey * ey) + P.r * phi * phi;
         const double rho2 = dxg * dxg + dyg * dyg;
         // (p = goal exactly: the target heading's derivatives are 0)
-        w.gfg[gx(k, 0)] = 2 * wk * ex + 2 * P.r * phi * (rho2 > 0.0 ? -dyg / rho2 : 0.0);
-        w.gfg[gx(k, 1)] = 2 * wk * ey + 2 * P.r * phi * (rho2 > 0.0 ? dxg / rho2 : 0.0);
+        // (explicit fma: the sweep kernel's copy of these sums must contract the same way)
+        const double q0 = rho2 > 0.0 ? -dyg / rho2 : 0.0, q1 = rho2 > 0.0 ? dxg / rho2 : 0.0;
+        w.gfg[gx(k, 0)] = fma(2 * P.r * phi, q0, 2 * wk * ex);
+        w.gfg[gx(k, 1)] = fma(2 * P.r * phi, q1, 2 * wk * ey);
         w.gfg[gx(k, 4)] = 2 * P.r * phi;
     }
     const double f = gsum16(fk);
@@ -2684,15 +2696,15 @@ __global__ __launch_bounds__(WAVE * WPG, 2) void sweep_kernel(KP Pv)
         // first firing circle's side picks the new heading (same functions, same values as eval_kernel)
         double gxg = g0, gyg = g1;
         if (P.detour) {
-            const double gd = (x0v[0] - g0) * (x0v[0] - g0) + (x0v[1] - g1) * (x0v[1] - g1);
-            const double th = atan2(g1 - x0v[1], g0 - x0v[0]);
+            const double gd = fma(x0v[0] - g0, x0v[0] - g0, (x0v[1] - g1) * (x0v[1] - g1));
+            const double th = latan2(g1 - x0v[1], g0 - x0v[0]);
             bool found = false;
             double na = 0.0;
 #pragma unroll
             for (int sl = 0; sl < NC; ++sl) {
                 const double* c = obs + 3 * sl;
-                const double cen = (x0v[0] - c[0]) * (x0v[0] - c[0]) + (x0v[1] - c[1]) * (x0v[1] - c[1]);
-                const double al = atan2(c[1] - x0v[1], c[0] - x0v[0]);
+                const double cen = fma(x0v[0] - c[0], x0v[0] - c[0], (x0v[1] - c[1]) * (x0v[1] - c[1]));
+                const double al = latan2(c[1] - x0v[1], c[0] - x0v[0]);
                 double dd = th - al;
                 if (dd < 0 && fabs(dd) > M_PI)
                     dd += 2 * M_PI;
@@ -2705,9 +2717,9 @@ __global__ __launch_bounds__(WAVE * WPG, 2) void sweep_kernel(KP Pv)
             if (found) {
                 const double rr = sqrt(gd);
                 double sn, cs;
-                sincos(na, &sn, &cs);
-                gxg = x0v[0] + rr * cs;
-                gyg = x0v[1] + rr * sn;
+                lsincos(na, &sn, &cs);
+                gxg = fma(rr, cs, x0v[0]);
+                gyg = fma(rr, sn, x0v[1]);
             }
         }
         // V = E x0 + G u over the structural non-zeros of G (x_k: u_0..u_{k-1}; p_k: u_0..u_k)
@@ -2751,8 +2763,9 @@ __global__ __launch_bounds__(WAVE * WPG, 2) void sweep_kernel(KP Pv)
             const double phi = th - latan2(dyg, dxg);
             fk[k] = wk * (ex * ex + ey * ey) + P.r * phi * phi;
             const double rho2 = dxg * dxg + dyg * dyg;
-            gfg[k][0] = 2 * wk * ex + 2 * P.r * phi * (rho2 > 0.0 ? -dyg / rho2 : 0.0);
-            gfg[k][1] = 2 * wk * ey + 2 * P.r * phi * (rho2 > 0.0 ? dxg / rho2 : 0.0);
+            const double q0 = rho2 > 0.0 ? -dyg / rho2 : 0.0, q1 = rho2 > 0.0 ? dxg / rho2 : 0.0;
+            gfg[k][0] = fma(2 * P.r * phi, q0, 2 * wk * ex);   // (eval_group_one's sums, contracted alike)
+            gfg[k][1] = fma(2 * P.r * phi, q1, 2 * wk * ey);
             gfg[k][2] = 2 * P.r * phi;
         }
         if (live) {
@@ -3561,7 +3574,7 @@ __global__ __launch_bounds__(256, dd_solve_waves<RPL>()) void dd_solve_kernel(KP
         } else {
             amin = gth;
         }
-        amin = uni(amin * gal);
+        amin = uni(fmax(amin * gal, 8.673617379884035e-19));   // (floor: DESIGN.md §2 item 8)
         // ---- filter line search: trial u = U + a dU, rolled out
         double a = ap;
         double la = uni(log(ap));
@@ -4810,7 +4823,7 @@ size_t smem_bytes(const Handle* h, bool solve)
         WSCASE(1) WSCASE(2) WSCASE(3) WSCASE(4) WSCASE(5) WSCASE(6)
 #undef WSCASE
     }
-    const int e = solve ? ((h->NG * 5 + 3) & ~3) : h->NG * 5 + ((h->NG * 5) & 1);
+    const int e = solve ? 0 : h->NG * 5 + ((h->NG * 5) & 1);   // (solve_kernel: E from global memory)
     const int ncp = solve ? h->NCP : h->NCPU;
     // KP in fp64 units, then G, E and the per-wave workspaces in the kernel's arithmetic type
     const size_t per_block = solve ? (size_t)WAVES_PER_BLOCK : (size_t)GROUPS_PER_BLOCK;   // workspaces

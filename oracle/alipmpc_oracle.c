@@ -1159,6 +1159,9 @@ static void osolve(oprob* P, const double* u0, double* uout, osolve_info* info)
         } else
             amin = gth;
         amin *= gal;
+        /* floor 2^-60: with theta = 0 exactly the formula gives 0, and a trial sequence
+           ap 2^-j never falls below it */
+        amin = fmax(amin, 8.673617379884035e-19);
         double a = ap;
         int accepted = 0, ftype = 0;
         while (a >= amin) {
