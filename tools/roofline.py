@@ -37,10 +37,15 @@ SIMDS, XCDS = 1024, 8
 
 
 def counters(d, kern, skip=1):
+    """Per-dispatch means of the kernel's counters over the dispatches of the benchmarked batch: the largest grid of
+    the family (bench.py's latency probe and feasibility checks launch the same kernel on small grids)."""
     acc = defaultdict(list)
     meta = {}
     for f in sorted(glob.glob(os.path.join(d, "pmc_*", "pmc_counter_collection.csv"))):
         rows = [r for r in csv.DictReader(open(f)) if r["Kernel_Name"].startswith(kern)]
+        if rows:
+            g = max(int(r["Grid_Size"]) for r in rows)
+            rows = [r for r in rows if int(r["Grid_Size"]) == g]
         ids = sorted({int(r["Dispatch_Id"]) for r in rows})[skip:]
         for r in rows:
             if int(r["Dispatch_Id"]) in ids:
@@ -52,7 +57,16 @@ def counters(d, kern, skip=1):
 
 def kernel_ms(d, kern, launches=1):
     """Mean duration per SOLVE of the kernel family: launches per solve x the mean dispatch (a split launch runs
-    phase 1 and phase 2 of every solve as two dispatches of the same kernel)."""
+    phase 1 and phase 2 of every solve as two dispatches of the same kernel).  From the per-dispatch trace when present,
+    restricted like counters() to the largest grid of the family; else the stats summary."""
+    for f in glob.glob(os.path.join(d, "prof_kt", "*kernel_trace.csv")):
+        rows = [r for r in csv.DictReader(open(f)) if r["Kernel_Name"].startswith(kern)]
+        if rows:
+            def gs(r):
+                return int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
+            g = max(gs(r) for r in rows)
+            dur = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows if gs(r) == g]
+            return launches * sum(dur) / len(dur) * 1e-6, len(dur)
     for f in glob.glob(os.path.join(d, "prof_kt", "*kernel_stats.csv")):
         for r in csv.DictReader(open(f)):
             if r["Name"].startswith(kern):
