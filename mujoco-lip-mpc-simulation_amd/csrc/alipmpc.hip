@@ -1187,6 +1187,12 @@ __device__ __forceinline__ R obj_sum(const R (&v)[RPL], int mr4)
     return s;
 }
 
+// team hand-over of the winning trial's values through LDS (instead of every other member re-evaluating it): when
+// they fit the KKT area of a workspace (3 row values per row slot + 3 scalars), which every iteration rewrites in
+// full before reading it (the Hessian-block area keeps a zero pattern across iterations, so not that one)
+template <int N, int RPL>
+constexpr bool TEAM_HANDOVER = 3 * WAVE * RPL + 3 <= Dim<N>::NCP * Dim<N>::KLD;
+
 // TM: the team-capable build (split launches with team records, solve_kernel<..., TM = true>): phase 1 also cuts an
 // instance by its line-search trial count, phase 2 runs team records on 4 waves; tm < 0 = member -1 - tm of a team.
 // Without TM all of it compiles out: the interior-point loop of the plain build sits at its register budget, and the
@@ -1973,6 +1979,40 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* wsb, int wv, lo
                 if (wn == 4) continue;
                 if (fw == 0) break;   // trial J + wn is below amin: no acceptable trial
                 ftype = fw == 3;
+                if constexpr (TEAM_HANDOVER<N, RPL>) {
+                    // hand-over: the winner's trial values (row values and transcendentals, f, the log sum, theta)
+                    // go to the others through the winner's KKT area, dead until the next iteration's K products; a
+                    // second barrier orders the reads before that overwrite
+                    R* hv = w.K + (wn - me) * wss;
+                    if (wn == me) {
+#pragma unroll
+                        for (int q = 0; q < RPL; ++q) {
+                            hv[(3 * q) * WAVE + lane] = ctr[q];
+                            hv[(3 * q + 1) * WAVE + lane] = ta0[q];
+                            hv[(3 * q + 2) * WAVE + lane] = ta1[q];
+                        }
+                        if (lane == 0) {
+                            hv[3 * RPL * WAVE] = ft;
+                            hv[3 * RPL * WAVE + 1] = lgt;
+                            hv[3 * RPL * WAVE + 2] = tht_acc;
+                        }
+                    }
+                    __syncthreads();
+                    if (wn != me) {
+#pragma unroll
+                        for (int q = 0; q < RPL; ++q) {
+                            ctr[q] = hv[(3 * q) * WAVE + lane];
+                            ta0[q] = hv[(3 * q + 1) * WAVE + lane];
+                            ta1[q] = hv[(3 * q + 2) * WAVE + lane];
+                        }
+                        ft = uni(hv[3 * RPL * WAVE]);
+                        lgt = uni(hv[3 * RPL * WAVE + 1]);
+                        tht_acc = uni(hv[3 * RPL * WAVE + 2]);
+                    }
+                    __syncthreads();
+                    accepted = true;
+                    break;
+                }
                 if (wn == me) {
                     accepted = true;
                     break;
