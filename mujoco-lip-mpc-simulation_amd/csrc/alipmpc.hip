@@ -1414,7 +1414,9 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* wsb, int wv, lo
         if (lane < NG) w.V[lane] = vme;
         wave_sync();
 #ifndef ALIP_NO_SETPRIO
-        if (it0 >= 20)
+        // (a team is the critical path of its launch by construction — the instance whose line searches ran long —
+        // and in the closed loop it shares SIMDs with the other episode group's phase 1: top priority)
+        if (it0 >= 20 || (TM && tm < 0))
             __builtin_amdgcn_s_setprio(3);
         else if (it0 >= 14)
             __builtin_amdgcn_s_setprio(2);
@@ -1475,7 +1477,9 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* wsb, int wv, lo
         // that have run long get priority, so the critical (high-iteration) instances run closer to their
         // lone-wave latency while the short ones, which have slack, yield.
 #ifndef ALIP_NO_SETPRIO
-        if (it == 8)
+        if (TM && tm < 0)
+            ;   // a team member keeps the top priority it resumed with
+        else if (it == 8)
             __builtin_amdgcn_s_setprio(1);
         else if (it == 14)
             __builtin_amdgcn_s_setprio(2);
@@ -1967,11 +1971,18 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* wsb, int wv, lo
                 }
                 __syncthreads();
                 const R* vt0 = w.Vt - me * wss;   // member 0's flags
-                int wn = 0, fw = 0;   // first member whose trial did not end in a rejection, and its flag
-                for (; wn < 4; ++wn) {
-                    fw = rfl((int)vt0[wn * wss + par]);
-                    if (fw != 1) break;
+                // first member whose trial did not end in a rejection, and its flag (the 4 flags read together)
+                int fl[4];
+#pragma unroll
+                for (int m = 0; m < 4; ++m) fl[m] = (int)vt0[m * wss + par];
+                int wn = 4, fw = 0;
+#pragma unroll
+                for (int m = 3; m >= 0; --m) {
+                    wn = fl[m] != 1 ? m : wn;
+                    fw = fl[m] != 1 ? fl[m] : fw;
                 }
+                wn = rfl(wn);
+                fw = rfl(fw);
                 for (int t = 0; t < wn; ++t) {   // a, la of trial J + wn (J + 4 when all four rejected)
                     a = uni(a * R(0.5));
                     la = uni(la - R(M_LN2));
