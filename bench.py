@@ -279,10 +279,10 @@ def main():
             },
             "roofline": {
                 "kernel": kname,
-                # wave program: a latency chain (MFMA busy ~0.05 of the SIMD cycles), see "latency"; lane program: vector
-                # issue of the fp64 KKT algebra
-                "bound": ("latency" if (prof.get("mfma_busy_share") is None or prof["mfma_busy_share"] < 0.1) else "mfma")
-                if program == "wave" else "valu",
+                # the binding resource from the counters of this build: MFMA busy (wave program ~0.05, never the bound),
+                # vector issue (>= half of the SIMD issue slots: cfg3's queue of 65,536 instances, the lane program) or
+                # else the latency chain of the slowest instances (cfg2, cfg1; see "latency")
+                "bound": bound_label(program, prof),
                 "latency": lat,
                 "achieved": achieved,
                 "peak": peak,
@@ -390,6 +390,18 @@ def counter_record(key, bid):
 
 CLOCK_GHZ = 2.4   # MI355X max engine clock (MI355X_MICROARCH.md); cycle figures below are at this clock
 ISSUE_CYC = 4     # one wave alone issues at most one instruction per 4 cycles (MI355X_MICROARCH.md: s_nop / v_fma 4)
+
+
+def bound_label(program, prof):
+    """Roofline bound of the solve kernel: "mfma" when the matrix cores are busy >= half the SIMD cycles, "valu" when
+    vector issue takes >= half the issue slots (and, without counters, for the lane program, whose fp64 KKT algebra runs
+    on the vector ALUs), else "latency" (the wave program's dependency chains)."""
+    mfma, valu = prof.get("mfma_busy_share"), prof.get("valu_issue_frac")
+    if mfma is not None and mfma >= 0.5:
+        return "mfma"
+    if (valu is not None and valu >= 0.5) or (valu is None and program == "lane"):
+        return "valu"
+    return "latency"
 
 
 def latency_probe(solver, inp, out, iters, prof, dev, copies=64, reps=5):
