@@ -261,3 +261,16 @@ def test_strong_scaling_inputs_identical_across_world_sizes_gloo():
     assert full.shape == ref.shape and np.array_equal(full, ref)
     # and every config runs one program whatever the world size
     assert all(c["program"] in ("wave", "lane") for c in bench.CONFIGS.values())
+
+
+def test_bench_bound_label_from_counters():
+    """The bench line's roofline `bound` is read off the profiled build's counters: the
+    cfg2 / cfg3 / cfg4 counter shares of profiles/r4/r4h, and the label without counters."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    assert bench.bound_label("wave", {"mfma_busy_share": 0.055, "valu_issue_frac": 0.464}) == "latency"   # cfg2
+    assert bench.bound_label("wave", {"mfma_busy_share": 0.089, "valu_issue_frac": 0.646}) == "valu"      # cfg3
+    assert bench.bound_label("lane", {"mfma_busy_share": 0.0, "valu_issue_frac": 0.396}) == "latency"     # cfg4
+    assert bench.bound_label("wave", {"mfma_busy_share": 0.6, "valu_issue_frac": 0.7}) == "mfma"
+    assert bench.bound_label("lane", {}) == "valu" and bench.bound_label("wave", {}) == "latency"
