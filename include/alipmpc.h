@@ -25,14 +25,15 @@
  *     is the split launch's record buffer (alipmpc_solve_launches): one per stream, made by the stream's first
  *     split solve, sized for the resident slots and kept until alipmpc_destroy — a capture on a stream that has
  *     none yet records the one-phase form.  A captured graph uses its capture stream's buffer: replay it on that
- *     stream (or ordered with the solves there).  At most 8 streams per handle hold one; a ninth stream takes
- *     over the least recently used buffer no capture has used.  ALIPMPC_STREAM_NULL selects device pointers on
+ *     stream (or ordered with the solves there).  At most 8 streams per handle hold one (kept until destroy, never
+ *     evicted); solves on a further stream run the one-phase form (same bits).  ALIPMPC_STREAM_NULL selects device pointers on
  *     the null (default) stream, whose handle value is 0.
  *   - Every LIP solve launch takes one of the handle's 64 work-queue counter pairs (a ring; each pair is
  *     reset by the last wave of the launch that used it).  A solve captured into a hipGraph bakes in one
  *     pair: do not replay such a graph concurrently with itself, and keep fewer than 64 solve launches of
  *     one handle in flight at once (across all streams), or two launches share counters and instances
- *     are skipped or solved twice.
+ *     are skipped or solved twice.  alipmpc_closed_loop_batch's ticks do not take ring pairs: each of its
+ *     episode groups owns one pair of its own (its launches run in order on the group's stream).
  *   - Row-major, instance-major arrays ("B x k" = k contiguous values per instance).
  *   - Return 0 on success, a negative ALIPMPC_E* code on error; alipmpc_last_error(h) gives the text.
  *   - There is no CPU execution path: a handle needs a visible gfx950 device.
@@ -72,6 +73,7 @@ extern "C" {
 #define ALIPMPC_INFEASIBLE_PROBLEM_DETECTED 2
 #define ALIPMPC_MAXIMUM_ITERATIONS_EXCEEDED (-1)
 #define ALIPMPC_ERROR_IN_STEP_COMPUTATION (-3)   /* KKT regularisation exhausted; last iterate returned */
+#define ALIPMPC_INVALID_NUMBER_DETECTED (-13)    /* cfg.goal_singular = ABORT only: see alipmpc_cfg */
 /* rollout only: the instance had already reached its goal, no solve was run at this step */
 #define ALIPMPC_ROLLOUT_DONE (-10)
 
@@ -122,7 +124,18 @@ typedef struct alipmpc_cfg {
                            (lane_kernel, throughput-optimised: batches of 10^5+ instances; N = 3 with circles only,
                            modi / sig_step, otherwise alipmpc_create returns ALIPMPC_EUNSUPPORTED).  A per-handle
                            choice, never a function of B: an instance's result does not depend on its batch. */
+    int32_t goal_singular; /* a planned state exactly on the goal, where the target heading atan2(g - p) has 0 / 0
+                           derivatives (the reference's cal_dtar_ang_du, MPC_LIP_modi.py:650-655, returns NaN there):
+                           ALIPMPC_GOAL_SINGULAR_ZERO (0, default) — take them as 0 (atan2(0, 0) = 0 held locally
+                           constant; a deviation); ALIPMPC_GOAL_SINGULAR_ABORT (1) — the
+                           reference's path: IPOPT's gradient check (Eval_Error on a non-finite objective gradient)
+                           ends the solve with status ALIPMPC_INVALID_NUMBER_DETECTED (-13) at the first iterate
+                           (starting point or accepted step) with such a state, and that iterate is returned.
+                           (Fills the struct's tail padding: sizeof(alipmpc_cfg) is unchanged.) */
 } alipmpc_cfg;
+
+#define ALIPMPC_GOAL_SINGULAR_ZERO 0
+#define ALIPMPC_GOAL_SINGULAR_ABORT 1
 
 /* Fill *out with the reference's constants for a variant and horizon.  nc_max = ne_max = 6, precision
  * fp64, max_iter = the reference's IPOPT cap (modi 30, sig_step 20, DD 40). */
@@ -283,6 +296,8 @@ int alipmpc_solve_slots(void* handle, int64_t* slots);
  * unfinished instances from their exact loop-state records — or, fp64, ALIPMPC_SPLIT_TR > 0), 1 otherwise; *team = 4
  * when phase 1 also cuts instances by their line-search trial count (ALIPMPC_SPLIT_TR > 0, fp64 only) into team
  * records that phase 2 runs on 4 waves each, else 1.
+ * It reports the form of an eager launch on a stream that holds, or can still get, a record buffer: a launch
+ * captured into a graph on a stream without one, or on a ninth stream, runs the one-phase form (1 launch).
  * Profiling tools use it to turn per-dispatch figures into per-solve ones.  No reference counterpart. */
 int alipmpc_solve_launches(void* handle, int64_t B, int32_t* launches, int32_t* team);
 

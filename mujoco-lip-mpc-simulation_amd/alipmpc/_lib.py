@@ -15,9 +15,12 @@ from . import build as _build
 VARIANT_MODI, VARIANT_SIG_STEP, VARIANT_DD = 0, 1, 2
 PREC_FP64, PREC_FP32 = 0, 1
 PROGRAM_WAVE, PROGRAM_LANE = 0, 1   # cfg.program: one instance per wavefront / per lane (include/alipmpc.h)
+GOAL_SINGULAR_ZERO, GOAL_SINGULAR_ABORT = 0, 1   # cfg.goal_singular (include/alipmpc.h)
+INVALID_NUMBER_DETECTED = -13
 
 STATUS_NAMES = {0: "Solve_Succeeded", 1: "Solved_To_Acceptable_Level", 2: "Infeasible_Problem_Detected",
                 -1: "Maximum_Iterations_Exceeded", -3: "Error_In_Step_Computation",
+                -13: "Invalid_Number_Detected (cfg.goal_singular = GOAL_SINGULAR_ABORT)",
                 -10: "Rollout_Done (goal reached earlier, not solved)"}
 ROLLOUT_DONE = -10
 
@@ -31,7 +34,7 @@ class Cfg(ctypes.Structure):
                [(k, ctypes.c_double) for k in
                 ("tol", "acceptable_tol", "dt", "H", "g", "leg2_max", "bvx_lo", "bvx_hi", "bvy_lo", "bvy_hi",
                  "dtheta_max", "q", "p", "r", "gamma", "s", "detect_r2", "dd_t", "mu_init")] + \
-               [("program", ctypes.c_int32)]
+               [("program", ctypes.c_int32), ("goal_singular", ctypes.c_int32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

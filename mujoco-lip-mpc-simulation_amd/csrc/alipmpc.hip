@@ -65,6 +65,7 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 // ------------------------------------------------------------------------------------------------
 struct KP {
     int nc_max, ne_max, rps, m_max, mr4, mo4, modi, max_iter, select_obs, detour;
+    int goal_abort;   // cfg.goal_singular == ABORT: an iterate with a planned state on the goal ends with status -13
     double tol, acc_tol, q, p, r, gm1, s, detect_r2, leg2, bvx_lo, bvx_hi, bvy_lo, bvy_hi, dth, mu_init, dt, dd_t;
     const double* G;   // NG x NCP
     const double* E;   // NG x 5
@@ -116,6 +117,7 @@ struct KP {
 };
 
 constexpr int KP_DOUBLES = (int)((sizeof(KP) + 15) / 16 * 2);
+constexpr int FAIL_GOAL = 1 << 16;   // solve_kernel's fail_it tag of a cfg.goal_singular = ABORT exit
 // split-launch record of one instance: per lane and row group the row state (slack, multipliers, inverse slack
 // distances, value, transcendentals, the 4 generator values), the filter entries (2 x 2) and the generator value
 // V[lane]; then 16 uniform values
@@ -1368,7 +1370,8 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* wsb, int wv, lo
     int nf = 0;
     R dw_last = R(0.0);
     int status = -1, it = 0, n_rest = 0;
-    int fail_it = -1, it_end = max_iter;   // Error_In_Step_Computation: iteration, and the loop's end
+    // Error_In_Step_Computation: iteration (+ FAIL_GOAL: Invalid_Number_Detected), and the loop's end
+    int fail_it = -1, it_end = max_iter;
     R e0 = INFINITY;
     R theta_c = R(0.0);
     bool theta_ok = false;
@@ -1575,6 +1578,21 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* wsb, int wv, lo
             const bool anyw = whi >= wlo;
             const R comp0 = anyw ? fmax(fabs(whi), fabs(wlo)) : R(0.0);
             e0 = uni(fmax(base_err, rcp_div(comp0, sc)));
+            // cfg.goal_singular = ABORT: the reference's gradient is NaN at this iterate (cal_dtar_ang_du,
+            // MPC_LIP_modi.py:650-655) and IPOPT's Eval_Error ends the solve: Invalid_Number_Detected, iterate kept
+            if (rfl(P.goal_abort)) {
+                bool at_goal = false;   // an OBJ row's state exactly on the goal
+#pragma unroll
+                for (int q = 0; q < RPL; ++q) {
+                    const R dxg = CK.gxg - rv[q][0], dyg = CK.gyg - rv[q][1];
+                    at_goal |= rtype[q] == R_OBJ && dxg * dxg + dyg * dyg == R(0);
+                }
+                if (__ballot(at_goal) != 0ull) {   // (ends the loop as a factorisation failure does, fail_it)
+                    fail_it = it + FAIL_GOAL;
+                    it_end = it;
+                    break;
+                }
+            }
             if (e0 <= w.cst[K_TOL]) {
                 status = 0;
                 break;
@@ -2137,14 +2155,17 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* wsb, int wv, lo
         WSTAMP_WRITE(b, it, n_rest);
         return;
     }
-    if (fail_it >= 0) {   // the last iterate, as IPOPT returns it with Error_In_Step_Computation
+    if (fail_it >= FAIL_GOAL) {   // cfg.goal_singular = ABORT: Invalid_Number_Detected at this iterate
+        status = -13;
+        it = fail_it - FAIL_GOAL;
+    } else if (fail_it >= 0) {   // the last iterate, as IPOPT returns it with Error_In_Step_Computation
         status = -3;
         it = fail_it;
     }
     // ---- status + outputs (violation measured on the reference's exact |.|)
     wave_sync();
     RELANE();
-    if (status != 0 && status != 2 && status != -3) {
+    if (status != 0 && status != 2 && status != -3 && status != -13) {
         R viol = R(0.0);
 #pragma unroll
         for (int q = 0; q < RPL; ++q) {
@@ -3421,6 +3442,7 @@ __global__ __launch_bounds__(256, dd_solve_waves<RPL>()) void dd_solve_kernel(KP
     for (it = 0; it <= max_iter; ++it) {
         // ---- row layout: Jacobian rows at the current point (OBJ rows: grad f_k + Hessian parts)
         RELANE();
+        bool at_goal = false;   // an OBJ row's state exactly on the goal (cfg.goal_singular)
 #pragma unroll
         for (int q = 0; q < RPL; ++q) {
             const int r = lane + WAVE * q;
@@ -3433,6 +3455,9 @@ __global__ __launch_bounds__(256, dd_solve_waves<RPL>()) void dd_solve_kernel(KP
             if (rtype[q] == D_OBJ) {
 #pragma unroll
                 for (int i = 0; i < 8; ++i) w.hobj[8 * rk[q] + i] = hx[i];
+                const double* sk = ST + DD_ST * rk[q];
+                const double dxg = w.cst[DK_GX] - sk[0], dyg = w.cst[DK_GY] - sk[1];
+                at_goal |= dxg * dxg + dyg * dyg == 0.0;
             }
         }
         wave_sync();
@@ -3464,6 +3489,11 @@ __global__ __launch_bounds__(256, dd_solve_waves<RPL>()) void dd_solve_kernel(KP
         const double sc = uni(fmax(100.0, nz / fmax(1.0, w.cst[DK_NBL])) / 100.0);
         const double base_err = uni(fmax(ru / sd, rcm));
         e0 = uni(fmax(base_err, comp0 / sc));
+        // cfg.goal_singular = ABORT (MPC_DD_sig_step.py:527-531 divides 0 by 0 here): Invalid_Number_Detected
+        if (rfl(P.goal_abort) && __ballot(at_goal) != 0ull) {
+            status = -13;
+            break;
+        }
         if (e0 <= w.cst[DK_TOL]) {
             status = 0;
             break;
@@ -3773,7 +3803,7 @@ __global__ __launch_bounds__(256, dd_solve_waves<RPL>()) void dd_solve_kernel(KP
     // ---- status + outputs (split rows measure the reference's f_en violation exactly)
     wave_sync();
     RELANE();
-    if (status != 0 && status != 2 && status != -3) {
+    if (status != 0 && status != 2 && status != -3 && status != -13) {
         double viol = 0.0;
 #pragma unroll
         for (int q = 0; q < RPL; ++q) {
@@ -4649,7 +4679,8 @@ struct Handle {
     // eval hook: the circle-slot count sweep_kernel runs with (-1: eval_kernel serves this configuration)
     int sweep_nc = -1;
     // work-queue counter pairs of persistent solve launches (a ring: launches in flight on different
-    // streams use different pairs; each pair is reset by the last wave of the launch that used it)
+    // streams use different pairs; each pair is reset by the last wave of the launch that used it), followed by
+    // MAXG pairs owned by the closed loop's episode groups (one per group)
     static constexpr unsigned NQ = 64;
     uint32_t* dq = nullptr;
     mutable std::atomic<unsigned> qi{0};
@@ -4669,19 +4700,15 @@ struct Handle {
     int split_it = 0;
     int split_tr = 0;   // phase-1 trial cut: an instance at this many line-search trials resumes as a team (0 = off)
     int cl_split_it = 0, cl_split_tr = 0;   // the closed loop's per-tick solves (ALIPMPC_CL_SPLIT_IT / _TR)
-    // Record buffers are sized ONCE for the resident slots (the largest batch that splits) and never reallocated, so a
-    // graph captured on a stream keeps a valid pointer whatever batch sizes run on that stream later.  At most
-    // SPLIT_STREAMS of them: a further stream takes over the least recently used buffer that no capture has used
-    // (freed first); when every buffer has been captured, the new stream runs the one-phase form.
+    // Record buffers are sized ONCE for the resident slots (the largest batch that splits) and never reallocated or
+    // freed before alipmpc_destroy, so a graph captured on a stream keeps a valid pointer whatever batch sizes run on
+    // that stream later.  At most SPLIT_STREAMS of them: a further stream runs the one-phase form.
     static constexpr size_t SPLIT_STREAMS = 8;
     struct SplitBuf {
         void* p = nullptr;
         size_t bytes = 0;
-        bool captured = false;   // used by a launch that was being captured: kept until destroy
-        unsigned long long used = 0;
     };
     std::map<hipStream_t, SplitBuf> split;
-    unsigned long long split_clock = 0;
     std::mutex split_mtx;
     // launch timing: a ring of event pairs, so a re-record never targets an event still pending on the
     // stream (that serialises the host with the previous launch)
@@ -4897,6 +4924,7 @@ KP make_kp(const Handle* h, long long B, bool solve)
     P.max_iter = c.max_iter;
     P.select_obs = c.select_obs;
     P.detour = c.detour;
+    P.goal_abort = c.goal_singular == ALIPMPC_GOAL_SINGULAR_ABORT;
     P.tol = c.tol;
     P.acc_tol = c.acceptable_tol;
     P.q = c.q;
@@ -5144,9 +5172,9 @@ int alipmpc_create(const alipmpc_cfg* cfg, int device, void** handle)
                hipMemcpy(*d, v.data(), v.size() * sizeof(double), hipMemcpyHostToDevice) == hipSuccess;
     };
     if (!up(&h->dGp, Gp) || !up(&h->dEp, Ep) || !up(&h->dGu, Gu) || !up(&h->dEu, Eu) ||
-        hipMalloc(&h->dq, 2 * Handle::NQ * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&h->dq, 2 * (Handle::NQ + Handle::MAXG) * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&h->dlk, 48 * sizeof(double)) != hipSuccess || hipMalloc(&h->dlkf, 48 * sizeof(float)) != hipSuccess ||
-        hipMemset(h->dq, 0, 2 * Handle::NQ * sizeof(uint32_t)) != hipSuccess ||
+        hipMemset(h->dq, 0, 2 * (Handle::NQ + Handle::MAXG) * sizeof(uint32_t)) != hipSuccess ||
         hipStreamCreateWithFlags(&h->own, hipStreamNonBlocking) != hipSuccess ||
         !create_events(h)) {
         alipmpc_destroy(h);
@@ -5224,23 +5252,16 @@ static void* split_buffer(Handle* h, hipStream_t st, size_t need, hipError_t& er
     auto it = h->split.find(st);
     if (it == h->split.end()) {
         if (capturing) return nullptr;   // no allocation inside a capture: the one-phase form
-        if (h->split.size() >= Handle::SPLIT_STREAMS) {
-            auto lru = h->split.end();
-            for (auto j = h->split.begin(); j != h->split.end(); ++j)
-                if (!j->second.captured && (lru == h->split.end() || j->second.used < lru->second.used)) lru = j;
-            if (lru == h->split.end()) return nullptr;   // every buffer belongs to a captured graph
-            // (hipFree waits for the work in flight that may still use it)
-            if (lru->second.p) (void)hipFree(lru->second.p);
-            h->split.erase(lru);
-        }
+        // every buffer is kept until alipmpc_destroy (an eviction's hipFree synchronised the device and
+        // could free a buffer another thread had just been handed); a stream beyond SPLIT_STREAMS runs the one-phase
+        // form, which computes the same bits
+        if (h->split.size() >= Handle::SPLIT_STREAMS) return nullptr;
         Handle::SplitBuf sb;
         if ((err = hipMalloc(&sb.p, need)) != hipSuccess) return nullptr;
         sb.bytes = need;
         it = h->split.emplace(st, sb).first;
     }
     if (it->second.bytes < need) return nullptr;   // (sized for the slots: does not happen)
-    it->second.captured |= capturing;
-    it->second.used = ++h->split_clock;
     return it->second.p;
 }
 
@@ -5747,7 +5768,10 @@ int alipmpc_closed_loop_batch(void* handle, int64_t B, int32_t S, int32_t f_cyc,
                     HIPCHK(h, hipGetLastError());
                     Pg.order = l.ord;
                 }
-                Pg.queue = h->dq + 2 * (h->qi.fetch_add(1u) % Handle::NQ);
+                // each group's own counter pair (after the ring): its launches run in order on its stream, and no
+                // other group or call can take the pair while one of them is in flight (ring pairs taken
+                // per tick let a group running ticks ahead land on a pair another group's launch still used)
+                Pg.queue = h->dq + 2 * (Handle::NQ + g);
 #ifdef ALIP_WSTAMP
                 {   // diagnostic record slots of this tick: (s f_cyc + i) B + instance
                     const long long base = ((long long)s * f_cyc + i) * B;

@@ -995,6 +995,29 @@ static void phess(const oprob* P, const double* pv, const double* y, double* Hp)
 
 
 
+/* a planned state exactly on the goal (rho2 = |g - p|^2 == 0), where the reference's cal_dtar_ang_du
+   (MPC_LIP_modi.py:650-655; MPC_DD_sig_step.py:527-531) divides 0 by 0 */
+static int at_goal(const oprob* P, const double* pv)
+{
+    if (P->dd) {
+        double X[OMAXN + 1][3];
+        dd_rollout(P, pv, X);
+        for (int k = 1; k <= P->N; ++k) {
+            double dxg = P->goal[0] - X[k][0], dyg = P->goal[1] - X[k][1];
+            if (dxg * dxg + dyg * dyg == 0.0) return 1;
+        }
+        return 0;
+    }
+    double u[OMAXV], X[OMAXN + 1][5], Pp[OMAXN][3];
+    u_of_p(P, pv, u);
+    rollout(P, u, X, Pp);
+    for (int k = 1; k <= P->N; ++k) {
+        double dxg = P->goal[0] - X[k][0], dyg = P->goal[1] - X[k][1];
+        if (dxg * dxg + dyg * dyg == 0.0) return 1;
+    }
+    return 0;
+}
+
 /* Primal-dual interior point with IPOPT's filter line search; mirrors np_oracle.solve. */
 static void osolve(oprob* P, const double* u0, double* uout, osolve_info* info)
 {
@@ -1041,6 +1064,12 @@ static void osolve(oprob* P, const double* u0, double* uout, osolve_info* info)
     double dl[OMAXM], du[OMAXM], rc[OMAXM], Sig[OMAXM], dU[OMAXV], dS[OMAXM], dZl[OMAXM], dZu[OMAXM];
     double ut[OMAXV], st[OMAXM], ct[OMAXM];
     for (it = 0; it <= cfg->max_iter; ++it) {
+        /* cfg.goal_singular = ABORT: the reference's NaN gradient at this iterate — IPOPT's Eval_Error, status
+           Invalid_Number_Detected with the iterate returned (include/alipmpc.h) */
+        if (cfg->goal_singular == ALIPMPC_GOAL_SINGULAR_ABORT && at_goal(P, u)) {
+            status = ALIPMPC_INVALID_NUMBER_DETECTED;
+            break;
+        }
         double f = pobj(P, u);
         pgrad(P, u, gf);
         pjac(P, u, J);
@@ -1159,9 +1188,9 @@ static void osolve(oprob* P, const double* u0, double* uout, osolve_info* info)
         } else
             amin = gth;
         amin *= gal;
-        /* floor 2^-60: with theta = 0 exactly the formula gives 0, and a trial sequence
-           ap 2^-j never falls below it */
-        amin = fmax(amin, 8.673617379884035e-19);
+        /* floor 2^-60 where the formula gives 0 (theta = 0 exactly): a trial sequence ap 2^-j
+           never falls below 0; a positive amin, however small, is IPOPT's own */
+        if (!(amin > 0.0)) amin = 8.673617379884035e-19;
         double a = ap;
         int accepted = 0, ftype = 0;
         while (a >= amin) {
@@ -1234,7 +1263,7 @@ static void osolve(oprob* P, const double* u0, double* uout, osolve_info* info)
 #undef ERR
     }
     free(ft);
-    if (status != 0 && status != 2 && status != -3) {
+    if (status != 0 && status != 2 && status != -3 && status != ALIPMPC_INVALID_NUMBER_DETECTED) {
         pcons(P, u, c);
         double viol = 0;
         for (int i = 0; i < m; ++i) {

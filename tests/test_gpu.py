@@ -1376,3 +1376,80 @@ def test_closed_loop_split_team_bit_identical(gpu_lib, variant, kick, B, prec, m
     for name, o in outs.items():
         for k in ref:
             assert np.array_equal(o[k], ref[k], equal_nan=True), (name, k)
+
+
+@pytest.mark.parametrize("program,prec,B", [(1, 1, 6000), (1, 0, 3000), (0, 0, 5000)])
+def test_closed_loop_groups_bit_identical(gpu_lib, program, prec, B, monkeypatch):
+    """Episode groups that do not divide the ring of work-queue pairs (ALIPMPC_CL_GROUPS = 3, 5, 7) on the programs
+    that take instances from the work queue every tick: the lane program, and the wave program on a batch above its
+    resident slots.  Each group owns a counter pair, so a group running ticks ahead of another never lands on a pair
+    still in use; every output equals the one-group loop's bit for bit."""
+    from alipmpc import scenes
+    S, F = 2, 40
+    bt = scenes.make_batch(B, seed=820 + program + 3 * prec, n_cir=5)
+    x0 = bt["x0"].copy()
+    x0[:300, 0:2] = bt["goal"][:300] - np.array([0.6, 0.5])
+    leg = bt["leg"].astype(np.int8)
+    kw = dict(nc_max=5, ne_max=0, program=program)
+    if prec:
+        kw["precision"] = gpu_lib.PREC_FP32
+    cfg = gpu_lib.default_cfg(0, 3, **kw)
+    s0 = gpu_lib.Solver(cfg)
+    if program == 0:
+        assert s0.solve_slots() < B
+    foot0 = s0.solve(x0, bt["goal"], leg, bt["cir"], bt["nc"], u0=np.tile(x0, (1, 3)))["foot"][:, 0:2]
+    outs = {}
+    for grp in ("1", "3", "5", "7"):
+        monkeypatch.setenv("ALIPMPC_CL_GROUPS", grp)
+        outs[grp] = gpu_lib.Solver(cfg).closed_loop(x0, foot0, bt["goal"], leg, bt["cir"], bt["nc"], steps=S, f_cyc=F,
+                                                    kick=0.05, seed=5)
+    ref = outs.pop("1")
+    assert (ref["status"] == 2).sum() > 0 and (ref["steps_to_goal"] > 0).sum() > 0
+    for name, o in outs.items():
+        for k in ref:
+            assert np.array_equal(o[k], ref[k], equal_nan=True), (name, k)
+
+
+@pytest.mark.parametrize("variant,program,prec", [(0, 0, 0), (1, 0, 0), (0, 0, 1), (0, 1, 0), (0, 1, 1), (1, 1, 1),
+                                                  (2, 0, 0)])
+def test_goal_singular_abort_matches_oracle(gpu_lib, coracle, variant, program, prec):
+    """cfg.goal_singular = ABORT: an instance starting ON the goal (x0 = goal, zero warm start: every
+    planned state exactly at the goal) ends as the reference's NaN gradient makes IPOPT end it — status -13
+    (Invalid_Number_Detected) at iteration 0 with the starting iterate — in every program, precision and variant,
+    as in the C oracle (tests/test_oracle.py::test_goal_singular_abort_semantics); the default (ZERO) solves on
+    there, and ordinary instances in the same batch are unaffected by the switch (bit-identical outputs)."""
+    from alipmpc import scenes
+    dd = variant == 2
+    N, B = 3, 64
+    n = 6 if dd else 15
+    bt = _dd_batch(B, seed=930, n_cir=3) if dd else scenes.make_batch(B, seed=930 + variant, n_cir=3)
+    x0, goal = bt["x0"].copy(), bt["goal"].copy()
+    x0[:8] = 0.0
+    goal[:8] = 0.0
+    u0 = bt["u0"].copy() if dd else np.tile(x0, (1, N))
+    u0[:8] = 0.0
+    kw = dict(nc_max=3, ne_max=0)
+    if program:
+        kw["program"] = gpu_lib.PROGRAM_LANE
+    if prec:
+        kw["precision"] = gpu_lib.PREC_FP32
+    outs = {}
+    for gs in (gpu_lib.GOAL_SINGULAR_ZERO, gpu_lib.GOAL_SINGULAR_ABORT):
+        s = gpu_lib.Solver(gpu_lib.default_cfg(variant, N, goal_singular=gs, **kw))
+        if dd:
+            outs[gs] = s.solve(x0, goal, None, bt["cir"], bt["nc"], u0=u0, last_u=bt["last_u"])
+        else:
+            outs[gs] = s.solve(x0, goal, bt["leg"], bt["cir"], bt["nc"], u0=u0)
+    a, z = outs[gpu_lib.GOAL_SINGULAR_ABORT], outs[gpu_lib.GOAL_SINGULAR_ZERO]
+    assert (a["status"][:8] == gpu_lib.INVALID_NUMBER_DETECTED).all() and (a["iters"][:8] == 0).all()
+    assert np.array_equal(a["u"][:8], np.zeros((8, n)))
+    assert (z["status"][:8] != gpu_lib.INVALID_NUMBER_DETECTED).all() and (z["iters"][:8] > 0).all()
+    for k in a:
+        assert np.array_equal(a[k][8:], z[k][8:], equal_nan=True), k
+    co = coracle.default_cfg(variant, N, nc_max=3, ne_max=0, goal_singular=gpu_lib.GOAL_SINGULAR_ABORT)
+    if dd:
+        r = coracle.solve_batch_dd(co, x0[:8], goal[:8], bt["cir"][:8], bt["nc"][:8], None, None, u0[:8],
+                                   bt["last_u"][:8])
+    else:
+        r = coracle.solve_batch(co, x0[:8], goal[:8], bt["leg"][:8], bt["cir"][:8], bt["nc"][:8], None, None, u0[:8])
+    assert np.array_equal(r["status"], a["status"][:8]) and np.array_equal(r["u"], a["u"][:8])

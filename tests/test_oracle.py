@@ -383,3 +383,40 @@ def test_goal_singularity_guard(golden, coracle, variant):
     r = coracle.solve_batch(cc, x0[None], goal[None], np.ones(1, np.int8), np.zeros((1, 0, 3)), np.zeros(1, np.int32),
                             None, None, u[None])
     assert r["status"][0] != -3 and np.isfinite(r["u"]).all()
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2])
+def test_goal_singular_abort_semantics(coracle, variant):
+    """cfg.goal_singular (include/alipmpc.h).  At a planned state exactly on the goal the reference's
+    cal_dtar_ang_du (MPC_LIP_modi.py:650-655, MPC_DD_sig_step.py:527-531) divides 0 by 0: its gradient is NaN, which
+    IPOPT's gradient evaluation rejects (Eval_Error) — Invalid_Number_Detected (-13) with that iterate returned.
+    GOAL_SINGULAR_ABORT reproduces that path in both oracles; the default (ZERO) takes the derivatives as 0 and solves
+    on.  The instance starts ON the singular point (x0 at the goal, zero warm start: every planned state at the goal
+    with exact arithmetic)."""
+    dd = variant == 2
+    N = 3
+    sd = 3 if dd else 5
+    n = 2 * N if dd else 5 * N
+    x0, goal, u0 = np.zeros(sd), np.zeros(2), np.zeros(n)
+    cir = np.array([[3.0, 3.0, 0.5]])
+    res = {}
+    for gs in (0, 1):
+        c = coracle.default_cfg(variant, N, nc_max=1, ne_max=0, goal_singular=gs)
+        o = O.default_cfg(variant, N, nc_max=1, ne_max=0, goal_singular=gs)
+        if dd:
+            r = coracle.solve_batch_dd(c, x0[None], goal[None], cir[None], np.ones(1, np.int32), None, None,
+                                       u0[None], np.zeros((1, 2)))
+            pu, pst, pit = O.dd_solve(O.DDProblem(o, x0, goal, cir, np.zeros((0, 5)), np.zeros(2)), u0)
+        else:
+            r = coracle.solve_batch(c, x0[None], goal[None], np.ones(1, np.int8), cir[None], np.ones(1, np.int32),
+                                    None, None, u0[None])
+            pu, pst, pit = O.solve_footholds(O.Problem(o, x0, goal, 1, cir, np.zeros((0, 5))), u0)
+        assert r["status"][0] == pst and r["iters"][0] == pit, (gs, r["status"][0], pst, r["iters"][0], pit)
+        res[gs] = (r, pu)
+    r1, pu1 = res[1]
+    assert r1["status"][0] == -13 and r1["iters"][0] == 0
+    # the starting iterate is returned (LIP: u_k = x_{k+1} of the zero footholds; DD: the controls)
+    assert np.array_equal(r1["u"][0], np.zeros(n)) and np.array_equal(pu1, np.zeros(n))
+    r0, pu0 = res[0]
+    assert r0["status"][0] != -13 and r0["iters"][0] > 0 and np.isfinite(r0["u"]).all()
+    assert np.abs(r0["u"][0] - pu0).max() <= 1e-6
