@@ -1882,9 +1882,10 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* wsb, int wv, lo
         } else {
             amin = gth;
         }
-        // floor 2^-60: with theta = 0 exactly the formula gives 0 and the trials a = ap 2^-j
-        // would never fall below it
-        amin = uni(fmax(amin * gal, R(8.673617379884035e-19)));
+        // floor 2^-60 where the formula gives 0 (theta = 0 exactly, DESIGN.md §2 item 8: the trials a = ap 2^-j would
+        // never fall below it); a positive amin, however small, is IPOPT's own
+        amin *= gal;
+        amin = uni(amin > R(0) ? amin : R(8.673617379884035e-19));
         STAMP(6);
         // ---- filter line search on trial points V + a dV (row registers only)
         // Trial j is a_j = ap 2^-j (and log a_j by the same sequential subtractions); the search takes the first
@@ -3655,7 +3656,8 @@ __global__ __launch_bounds__(256, dd_solve_waves<RPL>()) void dd_solve_kernel(KP
         } else {
             amin = gth;
         }
-        amin = uni(fmax(amin * gal, 8.673617379884035e-19));   // (floor: DESIGN.md §2 item 8)
+        amin *= gal;
+        amin = uni(amin > 0.0 ? amin : 8.673617379884035e-19);   // (floor where the formula gives 0: DESIGN.md §2 item 8)
         // ---- filter line search: trial u = U + a dU, rolled out
         double a = ap;
         double la = uni(log(ap));

@@ -995,9 +995,9 @@ def test_closed_loop_matches_oracle(gpu_lib, coracle, variant, kick, program, pr
         # and unconverged iterates differ; test_fp32_solve_vs_oracle's foothold bar on the converged touchdowns
         assert (o["steps_to_goal"] == ref["steps_to_goal"]).mean() >= 0.85
         assert conv.sum() >= 0.3 * B * S
-        # (measured r4: 0.83 within 1e-3, 0.71 within 1e-4, median 1.2e-5 — fp32 converges at tol 1e-4, and each tick
-        # warm-starts from the last fp32 plan)
-        assert (err[conv] <= 1e-3).mean() >= 0.8 and np.median(err[conv]) <= 1e-4, (err[conv] <= 1e-3).mean()
+        # (r4, map-frame fp32 heading error: 0.83 within 1e-3 — the fp32 floor near the goal; r5 with
+        # goal-frame positions and the heading error in fp64: see profiles/r5/parity)
+        assert (err[conv] <= 1e-3).mean() >= 0.9 and np.median(err[conv]) <= 1e-4, (err[conv] <= 1e-3).mean()
         np.testing.assert_allclose(o["hd"][:, 0], ref["hd"][:, 0], rtol=0, atol=1e-12)
         np.testing.assert_allclose(o["x"][:, 0], x0, rtol=0, atol=0)
         assert np.array_equal(np.isnan(o["action"]).all(-1), o["status"] == gpu_lib.ROLLOUT_DONE)
@@ -1014,7 +1014,9 @@ def test_closed_loop_matches_oracle(gpu_lib, coracle, variant, kick, program, pr
     # oracle's, median ~2e-14; the rest are episodes that drifted after a rounding-level change of path:
     # profiles/r4/parity/closed_loop_drift_*.json gives the tick where each of them leaves the oracle)
     assert (err[conv] <= 1e-3).mean() >= 0.9 and np.median(err[conv]) <= 1e-6
-    assert (err[conv] <= 1e-4).mean() >= 0.85, (err[conv] <= 1e-4).mean()
+    # (r5: 0.88, VERDICT r4 item 3 — the r4 drift tables put every drift at an unconverged or iteration-count-differing
+    # tick: measured 0.90-0.99)
+    assert (err[conv] <= 1e-4).mean() >= 0.88, (err[conv] <= 1e-4).mean()
     # every drift starts at an unconverged solve (iteration cap / infeasible: the returned iterate is path-dependent)
     # or where the iteration count differs (a warm start on the tolerance boundary), never inside a converged solve
     # that took the same iterations (r4 measurement: profiles/r4/parity/closed_loop_drift_*.json)
@@ -1070,10 +1072,24 @@ def test_closed_loop_step_failures_vs_oracle(gpu_lib, coracle, program, prec):
     o = s.closed_loop(x0, foot0, bt["goal"], leg, bt["cir"], bt["nc"], steps=1, f_cyc=F)
     ref = coracle.closed_loop_batch(coracle.default_cfg(0, 3, nc_max=5, ne_max=0), x0, foot0, bt["goal"], leg,
                                     bt["cir"], bt["nc"], steps=1, f_cyc=F, nthreads=16)
+    # the comparator at the program's own tolerances (fp32: tol 1e-4 / acceptable 1e-3), so that precision effects
+    # are told from tolerance effects
+    c = s.cfg
+    same = coracle.closed_loop_batch(coracle.default_cfg(0, 3, nc_max=5, ne_max=0, tol=c.tol,
+                                                         acceptable_tol=c.acceptable_tol), x0, foot0, bt["goal"], leg,
+                                     bt["cir"], bt["nc"], steps=1, f_cyc=F, nthreads=16) if prec else ref
     cnt = lambda st: {str(k): int(v) for k, v in zip(*np.unique(st[st != -10], return_counts=True))}  # noqa: E731
     _artifact(f"closed_loop_m3_{program}_{prec}.json", {"episodes": B, "ticks": int((o["status"] != -10).sum()),
-                                                        "gpu": cnt(o["status"]), "oracle": cnt(ref["status"])})
+                                                        "gpu": cnt(o["status"]), "oracle": cnt(ref["status"]),
+                                                        "oracle_same_tol": cnt(same["status"])})
     assert (o["status"] == -3).sum() <= (ref["status"] == -3).sum(), (cnt(o["status"]), cnt(ref["status"]))
+    # iteration-cap stops and converged ticks as the same-tolerance oracle's (r4's fp32 loop: 3x the cap stops, 74 %
+    # vs 91 % converged — the fp32 heading error near the goal)
+    ran = o["status"] != -10
+    n_cap, n_cap_ref = (o["status"] == -1).sum(), (same["status"] == -1).sum()
+    assert n_cap <= 1.25 * n_cap_ref + 20, (cnt(o["status"]), cnt(same["status"]))
+    assert (o["status"][ran] == 0).mean() >= (same["status"][ran] == 0).mean() - 0.03, (cnt(o["status"]),
+                                                                                        cnt(same["status"]))
     # the episodes near the goal reach it: the singular region is exercised
     assert (o["steps_to_goal"][near] > 0).sum() > 0
 
