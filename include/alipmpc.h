@@ -293,9 +293,9 @@ int alipmpc_solve_slots(void* handle, int64_t* slots);
 
 /* Kernel launches one alipmpc_solve_batch of B instances runs on this handle: 2 for a split launch (wave program,
  * 2 <= B <= alipmpc_solve_slots, and ALIPMPC_SPLIT_IT > 0 — phase 1 up to that many iterations, phase 2 resumes the
- * unfinished instances from their exact loop-state records — or, fp64, ALIPMPC_SPLIT_TR > 0), 1 otherwise; *team = 4
- * when phase 1 also cuts instances by their line-search trial count (ALIPMPC_SPLIT_TR > 0, fp64 only) into team
- * records that phase 2 runs on 4 waves each, else 1.
+ * unfinished instances from their exact loop-state records — or, fp64, ALIPMPC_SPLIT_TR > 0), 1 otherwise; *team = the
+ * team size (4 waves) when phase 1 also cuts instances by their line-search trial count (ALIPMPC_SPLIT_TR > 0, fp64
+ * only) into team records that phase 2 runs on a team each, else 1.
  * It reports the form of an eager launch on a stream that holds, or can still get, a record buffer: a launch
  * captured into a graph on a stream without one, or on a ninth stream, runs the one-phase form (1 launch).
  * Profiling tools use it to turn per-dispatch figures into per-solve ones.  No reference counterpart. */

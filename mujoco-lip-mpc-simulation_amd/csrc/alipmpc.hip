@@ -140,6 +140,14 @@ static int env_groups()
 constexpr int CONT_SINGLE = 0, CONT_TEAM = 1;
 __host__ __device__ constexpr long long cont_hdr(long long) { return 2; }
 constexpr long long TEAM_CAP = 128;   // team workgroups of a phase-2 launch (team records beyond run one wave each)
+// waves of a team-capable workgroup = members of a team, each testing one of that many consecutive line-search trials
+// per round.  r5 measured 8 against 4: the closed loop 33.8 vs 31.1 ms — every member also
+// runs the whole direction computation, and 8 of them share their SIMDs with the other episode group's phase 1
+// (profiles/r5/closed_loop); 4 kept
+#ifndef ALIP_TEAM_WAVES
+#define ALIP_TEAM_WAVES 4
+#endif
+constexpr int TEAM_WAVES = ALIP_TEAM_WAVES;
 #ifndef ALIP_GJ_REGS
 #define ALIP_GJ_REGS 1
 #endif
@@ -1990,23 +1998,23 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* wsb, int wv, lo
                 }
                 __syncthreads();
                 const R* vt0 = w.Vt - me * wss;   // member 0's flags
-                // first member whose trial did not end in a rejection, and its flag (the 4 flags read together)
-                int fl[4];
+                // first member whose trial did not end in a rejection, and its flag (the members' flags read together)
+                int fl[TEAM_WAVES];
 #pragma unroll
-                for (int m = 0; m < 4; ++m) fl[m] = (int)vt0[m * wss + par];
-                int wn = 4, fw = 0;
+                for (int m = 0; m < TEAM_WAVES; ++m) fl[m] = (int)vt0[m * wss + par];
+                int wn = TEAM_WAVES, fw = 0;
 #pragma unroll
-                for (int m = 3; m >= 0; --m) {
+                for (int m = TEAM_WAVES - 1; m >= 0; --m) {
                     wn = fl[m] != 1 ? m : wn;
                     fw = fl[m] != 1 ? fl[m] : fw;
                 }
                 wn = rfl(wn);
                 fw = rfl(fw);
-                for (int t = 0; t < wn; ++t) {   // a, la of trial J + wn (J + 4 when all four rejected)
+                for (int t = 0; t < wn; ++t) {   // a, la of trial J + wn (J + TEAM_WAVES when all rejected)
                     a = uni(a * R(0.5));
                     la = uni(la - R(M_LN2));
                 }
-                if (wn == 4) continue;
+                if (wn == TEAM_WAVES) continue;
                 if (fw == 0) break;   // trial J + wn is below amin: no acceptable trial
                 ftype = fw == 3;
                 if constexpr (TEAM_HANDOVER<N, RPL>) {
@@ -2249,8 +2257,9 @@ constexpr int solve_waves() { return 4 * KSM > WAVE ? ALIP_WAVES_RPL2 : (sizeof(
 // above the slots whole and in half-slot chunks and compares status, iters, u, foot, x_pred exactly), so an
 // instance's result does not depend on its batch or on the device's slot count.
 template <int N, int KSM, class R, bool ONE, bool TM = false>
-__global__ __launch_bounds__(256, (solve_waves<KSM, R>())) void solve_kernel(KP Pv)
+__global__ __launch_bounds__(WAVE * (TM ? TEAM_WAVES : WAVES_PER_BLOCK), (solve_waves<KSM, R>())) void solve_kernel(KP Pv)
 {
+    constexpr int WPB = TM ? TEAM_WAVES : WAVES_PER_BLOCK;   // waves per workgroup (team-capable: the team size)
     using D = Dim<N>;
     constexpr int NCP = D::NCP;
     constexpr int NG = D::NG;
@@ -2267,11 +2276,12 @@ __global__ __launch_bounds__(256, (solve_waves<KSM, R>())) void solve_kernel(KP 
     // slot k of the launch (wave k, or the k-th queue ticket) solves instance order[k] (identity without an order):
     // the per-instance arithmetic does not depend on the slot, only when and where the instance runs
     if constexpr (ONE) {
-        // split phase 2 of the team-capable build: workgroups [0, Pv.team) resume team records (the workgroup's 4 waves
-        // in lockstep on one instance), the rest single records one wave each, then any team records beyond Pv.team
+        // split phase 2 of the team-capable build: workgroups [0, Pv.team) resume team records (the workgroup's WPB
+        // waves in lockstep on one instance), the rest single records one wave each, then any team records beyond
+        // Pv.team
         const long long nteamwg = TM && Pv.resume ? (long long)Pv.team : 0;
         const bool team = (long long)blockIdx.x < nteamwg;
-        const long long k = team ? (long long)blockIdx.x : ((long long)blockIdx.x - nteamwg) * WAVES_PER_BLOCK + wv;
+        const long long k = team ? (long long)blockIdx.x : ((long long)blockIdx.x - nteamwg) * WPB + wv;
         long long b = -1, rec = -1;   // one inlined solve_one for every form (the code is large)
         if (Pv.resume) {   // split launch, phase 2
             const long long made = TM ? (long long)__builtin_amdgcn_readfirstlane(Pv.cont[CONT_TEAM]) : 0;
@@ -4438,16 +4448,29 @@ static unsigned resident_blocks(const void* f, size_t smem, int threads = WAVE *
     return r;
 }
 
+// the team-capable build's workgroup LDS: smem (KP, G and WAVES_PER_BLOCK workspaces) with TEAM_WAVES workspaces
+template <int N, class R>
+size_t team_smem(size_t smem)
+{
+    const size_t fixed = sizeof(double) * (size_t)KP_DOUBLES + sizeof(R) * (size_t)Dim<N>::NG * Dim<N>::NCP;
+    return fixed + (smem - fixed) / WAVES_PER_BLOCK * TEAM_WAVES;
+}
+
 template <int N, class R>
 void launch_solve(const KP& P0, size_t smem, hipStream_t st, unsigned* res_out)
 {
-    // (a split phase 2 of the team-capable build: P0.team team workgroups ahead of the one-wave-per-instance ones)
-    const unsigned need = (P0.resume ? (unsigned)P0.team : 0u) + (unsigned)((P0.B + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
+    const unsigned need = (unsigned)((P0.B + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
+    // a split launch with team records (team-capable build, TEAM_WAVES-wave workgroups); phase 2: P0.team team
+    // workgroups ahead of the one-wave-per-instance ones
+    const unsigned need_t = (P0.resume ? (unsigned)P0.team : 0u) + (unsigned)((P0.B + TEAM_WAVES - 1) / TEAM_WAVES);
+    const size_t smem_t = team_smem<N, R>(smem);
     // KSM = 4-row steps of the J layout, the smallest compiled size covering mo4 rows
     auto go = [&](auto kq, auto k1, auto kt) {
         set_smem((const void*)kq, smem);
         set_smem((const void*)k1, smem);
-        set_smem((const void*)kt, smem);
+        // (the team-capable build runs only where its workgroup fits the LDS: alipmpc_create clears the trial cuts
+        // otherwise)
+        if (smem_t <= 160 * 1024) set_smem((const void*)kt, smem_t);
         const unsigned res = resident_blocks((const void*)kq, smem);
         if (res_out) {   // query only (alipmpc_solve_slots)
             *res_out = res;
@@ -4456,7 +4479,7 @@ void launch_solve(const KP& P0, size_t smem, hipStream_t st, unsigned* res_out)
         if (res > 0 && need > res && !P0.resume)   // the persistent work queue over the resident workgroups
             hipLaunchKernelGGL(kq, dim3(res), dim3(WAVE * WAVES_PER_BLOCK), smem, st, P0);
         else if (P0.team > 0)        // a split launch with team records: both phases on the team-capable build
-            hipLaunchKernelGGL(kt, dim3(need > 0 ? need : 1u), dim3(WAVE * WAVES_PER_BLOCK), smem, st, P0);
+            hipLaunchKernelGGL(kt, dim3(need_t > 0 ? need_t : 1u), dim3(WAVE * TEAM_WAVES), smem_t, st, P0);
         else                         // every instance has a resident wave: one instance per wave
             hipLaunchKernelGGL(k1, dim3(need > 0 ? need : 1u), dim3(WAVE * WAVES_PER_BLOCK), smem, st, P0);
     };
@@ -5222,6 +5245,17 @@ int alipmpc_create(const alipmpc_cfg* cfg, int device, void** handle)
     if (smem_bytes(h, true) > 160 * 1024 || smem_bytes(h, false) > 160 * 1024) {
         alipmpc_destroy(h);
         return ALIPMPC_EUNSUPPORTED;
+    }
+    // team records need the team-capable build's TEAM_WAVES workspaces in one workgroup: without room, no trial cut
+    if (cfg->variant != ALIPMPC_VARIANT_DD && cfg->precision != ALIPMPC_PREC_FP32 && h->lane_nct < 0) {
+        size_t st_ = 0;
+        switch (h->N) {
+#define TSCASE(NN) \
+    case NN: st_ = team_smem<NN, double>(smem_bytes(h, true)); break;
+            TSCASE(1) TSCASE(2) TSCASE(3) TSCASE(4) TSCASE(5) TSCASE(6)
+#undef TSCASE
+        }
+        if (st_ > 160 * 1024) h->split_tr = h->cl_split_tr = 0;
     }
     *handle = h;
     return ALIPMPC_OK;
@@ -6007,7 +6041,7 @@ int alipmpc_solve_launches(void* handle, int64_t B, int32_t* launches, int32_t* 
     // launch_solve's conditions for the split form (no order / active mask on the batch API)
     const bool split = split_form(h, B, h->split_it, h->split_tr, slots);
     *launches = split ? 2 : 1;
-    *team = split && h->split_tr > 0 && h->cfg.precision != ALIPMPC_PREC_FP32 ? 4 : 1;
+    *team = split && h->split_tr > 0 && h->cfg.precision != ALIPMPC_PREC_FP32 ? TEAM_WAVES : 1;
     return ALIPMPC_OK;
 }
 

@@ -89,7 +89,8 @@ def main():
 
     # host-driven loop: GPU fp32 solves; every tick's inputs also solved by the oracle at the fp32 tolerances
     orig = C.solve_batch
-    rows = {k: [] for k in ("ep", "tick", "gst", "git", "ost", "oit", "dgoal", "dplan", "ferr", "o64st")}
+    rows = {k: [] for k in ("ep", "tick", "gst", "git", "ost", "oit", "dgoal", "dplan", "ferr", "o64st", "dbg")}
+    dbg = "dbg" in os.environ.get("ALIPMPC_LIB", "")   # the -DALIP_LANE_DBG build: x_pred[:8] = convergence terms
     tick = [0]
 
     def gpu_solve(cfg, x0, goal, leg_, cir, nc, elp, ne, u0, nthreads=1):
@@ -104,6 +105,9 @@ def main():
         rows["dgoal"].append(np.hypot(*(x0[:, 0:2] - goal).T))
         rows["dplan"].append(np.hypot(*(ro["x_pred"][:, -1, 0:2] - goal).T))
         rows["ferr"].append(np.abs(r["foot"] - ro["foot"]).max(-1))
+        if dbg:
+            rows["dbg"].append(r["x_pred"].reshape(len(x0), -1)[:, :8].copy())
+            r["x_pred"] = ro["x_pred"]   # (the driver's heading bookkeeping reads x_pred: take the oracle's)
         tick[0] += 1
         return r
     C.solve_batch = gpu_solve
