@@ -1364,6 +1364,48 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* wsb, int wv, lo
     }
     wsum2(th0, nbl);
     lg0 = wsum(lg0);
+    // IPOPT's default NLP scaling at the starting point (nlp_scaling_method = gradient-based; the reference sets no
+    // scaling option, MPC_LIP_modi.py:274-296): the OBJ rows' gradient on (px, py, theta) of x_k, taken to the
+    // reference's u through Gu (d x_k / d u), and the objective scaled by 100 / max |grad f| where that exceeds 100 —
+    // the objective is linear in its weights, so the weights are scaled (constraint rows' gradients stay below 4 in u:
+    // no row scaling)
+    {
+#pragma unroll
+        for (int q = 0; q < RPL; ++q) {
+            if (rtype[q] == R_OBJ) {
+                R o[6] = {R(0), R(0), R(0), R(0), R(0), R(0)}, cf[4], hx[6];
+                row_coef(R_OBJ, rk[q], rv[q], ra0[q], ra1[q], o, CK, cf, hx);
+                const int k = rk[q] - 1;
+                w.Vt[3 * k] = cf[0];
+                w.Vt[3 * k + 1] = cf[1];
+                w.Vt[3 * k + 2] = cf[2];
+            }
+        }
+        wave_sync();
+        R gu = R(0);
+        if (lane < D::nu) {
+#pragma unroll
+            for (int k = 1; k <= N; ++k) {
+                const double* gr = P.Gu + (size_t)(8 * k) * D::NCPU + lane;
+                gu += w.Vt[3 * (k - 1)] * (R)gr[0] + w.Vt[3 * (k - 1) + 1] * (R)gr[D::NCPU] +
+                      w.Vt[3 * (k - 1) + 2] * (R)gr[4 * D::NCPU];
+            }
+        }
+        const R gm = wmax(fabs(gu));
+        const R dfo = uni(gm > R(100) ? fmax(R(1e-8), R(100) / gm) : R(1));
+        wave_sync();
+        if (dfo != R(1)) {
+            if (lane == 0) {
+                w.cst[K_Q] *= dfo;
+                w.cst[K_P] *= dfo;
+                w.cst[K_R] *= dfo;
+            }
+#pragma unroll
+            for (int q = 0; q < RPL; ++q)
+                if (rtype[q] == R_OBJ) cr[q] *= dfo;
+            wave_sync();
+        }
+    }
     fo = obj_sum<N, RPL>(cr, mr4);
     mal = wsum(mal);
     R f_cur = fo, lsum_cur = lg0;
@@ -1689,12 +1731,17 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* wsb, int wv, lo
                 const R* Srow = w.S + 64 * kb + 8 * c;
                 const R* Gb = G + 8 * kb * NCP;
                 R gv[NT], sgv[NT];
+                // S rows 0..3 (even s: t & 7 = g4) have nonzeros in columns {0, 1, 4, 5, 6} only, rows 4..7 in {0..6}
+                // (hess_blocks' pattern; the rest of S stays zero): the zero products are skipped (+0 terms, the same
+                // sums)
+                const unsigned SCOLS = (s & 1) ? 0x7Fu : 0x73u;   // (s is unrolled: a constant per step)
 #pragma unroll
                 for (int T = 0; T < NT; ++T) {
                     gv[T] = G[t * NCP + 16 * T + col];
                     R a = R(0.0);
 #pragma unroll
-                    for (int c2 = 0; c2 < 8; ++c2) a += Srow[c2] * Gb[c2 * NCP + 16 * T + col];
+                    for (int c2 = 0; c2 < 8; ++c2)
+                        if ((SCOLS >> c2) & 1u) a += Srow[c2] * Gb[c2 * NCP + 16 * T + col];
                     sgv[T] = a;
                 }
                 auto* a = acc[s & 1];
@@ -3432,6 +3479,41 @@ __global__ __launch_bounds__(256, dd_solve_waves<RPL>()) void dd_solve_kernel(KP
         if (t < D_NONE) th0 += fabs(cr[q] - sr[q]);
         if (t == D_OBJ) fo += cr[q];
     }
+    // IPOPT's default NLP scaling at the starting point (MPC_DD_sig_step.py:176-190 sets no scaling option): the
+    // objective's gradient in u (the OBJ rows' Jacobian rows), the objective scaled by 100 / max |grad f| where that
+    // exceeds 100 — all four weights, the objective being linear in them
+    {
+#pragma unroll
+        for (int q = 0; q < RPL; ++q) {
+            const int r = lane + WAVE * q;
+            if (rtype[q] == D_OBJ) {
+                double o[6] = {0, 0, 0, 0, 0, 0}, hxs[8];
+                (void)dd_row<N, true>(D_OBJ, rk[q], o, w.cst, ST, U, w.Jd + 16 * r, hxs);
+            }
+        }
+        wave_sync();
+        double gu = 0.0;
+        if (lane < n) {
+#pragma unroll
+            for (int k = 0; k < N; ++k) gu += w.Jd[16 * (mr4 + k) + lane];
+        }
+        const double gm = wmax(fabs(gu));
+        const double dfo = uni(gm > 100.0 ? fmax(1e-8, 100.0 / gm) : 1.0);
+        wave_sync();
+        if (dfo != 1.0) {
+            if (lane == 0) {
+                w.cst[DK_Q] *= dfo;
+                w.cst[DK_P] *= dfo;
+                w.cst[DK_R] *= dfo;
+                w.cst[DK_TT] *= dfo;
+            }
+            fo *= dfo;
+#pragma unroll
+            for (int q = 0; q < RPL; ++q)
+                if (rtype[q] == D_OBJ) cr[q] *= dfo;
+            wave_sync();
+        }
+    }
     wsum2(th0, nbl);
     wsum2(fo, lg0);
     mal = wsum(mal);
@@ -4842,7 +4924,8 @@ void build_tables(const alipmpc_cfg& cfg, int NCPP, int NCPU, std::vector<double
 void lane_constants(const alipmpc_cfg& cfg, double* lk)
 {
     using namespace alip::lane;
-    for (int i = 0; i < 48; ++i) lk[i] = 0.0;
+    static_assert(LK_COUNT <= LK_BUF, "lane constants fit their buffer");
+    for (int i = 0; i < LK_BUF; ++i) lk[i] = 0.0;
     const double b = std::sqrt(cfg.g / cfg.H), T = cfg.dt;
     const double ch = std::cosh(b * T), sh = std::sinh(b * T);
     lk[LK_CH] = ch;
@@ -4891,6 +4974,27 @@ void lane_constants(const alipmpc_cfg& cfg, double* lk)
     lk[LK_ACC] = cfg.acceptable_tol;
     lk[LK_MU0] = cfg.mu_init;
     lk[LK_DET2] = cfg.detect_r2;
+    // d px_{k+1+m} / d u_k[px], [vx] of the reference's u (per axis: (MA^m MB)[0][0], [0][1], MA = (I - B W) A, MB = B W),
+    // for IPOPT's objective scaling at the starting point (lane_solve.inc)
+    {
+        const double Ax[2][2] = {{ch, sh / b}, {sh * b, ch}}, Bx[2] = {1.0 - ch, -sh * b};
+        const double Wx[2] = {lk[LK_WCH], lk[LK_WSH]};
+        double MA[2][2], MB[2][2], Mm[2][2] = {{1, 0}, {0, 1}};   // Mm = MA^m
+        for (int i = 0; i < 2; ++i)
+            for (int j = 0; j < 2; ++j) {
+                MB[i][j] = Bx[i] * Wx[j];
+                MA[i][j] = Ax[i][j] - Bx[i] * (Wx[0] * Ax[0][j] + Wx[1] * Ax[1][j]);
+            }
+        for (int m = 0; m < 6; ++m) {
+            lk[LK_SU0 + m] = Mm[0][0] * MB[0][0] + Mm[0][1] * MB[1][0];
+            lk[LK_SU1 + m] = Mm[0][0] * MB[0][1] + Mm[0][1] * MB[1][1];
+            double T[2][2];
+            for (int i = 0; i < 2; ++i)
+                for (int j = 0; j < 2; ++j) T[i][j] = Mm[i][0] * MA[0][j] + Mm[i][1] * MA[1][j];
+            for (int i = 0; i < 2; ++i)
+                for (int j = 0; j < 2; ++j) Mm[i][j] = T[i][j];
+        }
+    }
 }
 
 // the compiled lane-solver instance (circle slots) serving cfg, or -1 when none does: N = 3 with circles
@@ -5198,7 +5302,8 @@ int alipmpc_create(const alipmpc_cfg* cfg, int device, void** handle)
     };
     if (!up(&h->dGp, Gp) || !up(&h->dEp, Ep) || !up(&h->dGu, Gu) || !up(&h->dEu, Eu) ||
         hipMalloc(&h->dq, 2 * (Handle::NQ + Handle::MAXG) * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc(&h->dlk, 48 * sizeof(double)) != hipSuccess || hipMalloc(&h->dlkf, 48 * sizeof(float)) != hipSuccess ||
+        hipMalloc(&h->dlk, alip::lane::LK_BUF * sizeof(double)) != hipSuccess ||
+        hipMalloc(&h->dlkf, alip::lane::LK_BUF * sizeof(float)) != hipSuccess ||
         hipMemset(h->dq, 0, 2 * (Handle::NQ + Handle::MAXG) * sizeof(uint32_t)) != hipSuccess ||
         hipStreamCreateWithFlags(&h->own, hipStreamNonBlocking) != hipSuccess ||
         !create_events(h)) {
@@ -5206,10 +5311,10 @@ int alipmpc_create(const alipmpc_cfg* cfg, int device, void** handle)
         return ALIPMPC_EHIP;
     }
     {
-        double lk[48];
-        float lkf[48];
+        double lk[alip::lane::LK_BUF];
+        float lkf[alip::lane::LK_BUF];
         lane_constants(h->cfg, lk);
-        for (int i = 0; i < 48; ++i) lkf[i] = (float)lk[i];
+        for (int i = 0; i < alip::lane::LK_BUF; ++i) lkf[i] = (float)lk[i];
         if (hipMemcpy(h->dlk, lk, sizeof(lk), hipMemcpyHostToDevice) != hipSuccess ||
             hipMemcpy(h->dlkf, lkf, sizeof(lkf), hipMemcpyHostToDevice) != hipSuccess) {
             alipmpc_destroy(h);

@@ -53,6 +53,7 @@ typedef struct {
     double eqa[OMAXO], eqb[OMAXO], eqc[OMAXO], ek[OMAXO];
     int sel_c[OMAXO], sel_e[OMAXO];
     double cl[OMAXM], cu[OMAXM];
+    double df;   /* IPOPT's gradient-based objective scaling of the solve (osolve; 1 for the callbacks) */
 } oprob;
 
 /* ------------------------------------------------------------------------------------------------ */
@@ -196,6 +197,7 @@ static void oprob_init(oprob* P, const alipmpc_cfg* cfg, const oconsts* K, const
     P->n = 5 * cfg->N;
     P->modi = cfg->variant == ALIPMPC_VARIANT_MODI;
     P->split = split && P->modi;
+    P->df = 1.0;
     memcpy(P->x0, x0, 5 * sizeof(double));
     P->goal_orig[0] = goal[0];
     P->goal_orig[1] = goal[1];
@@ -640,6 +642,7 @@ static void oprob_init_dd(oprob* P, const alipmpc_cfg* cfg, const double* x0, co
     P->n = 2 * cfg->N;
     P->dd = 1;
     P->split = split;
+    P->df = 1.0;
     memcpy(P->x0, x0, 3 * sizeof(double));
     P->goal[0] = P->goal_orig[0] = goal[0];
     P->goal[1] = P->goal_orig[1] = goal[1];
@@ -916,12 +919,13 @@ static void u_of_p(const oprob* P, const double* pv, double* u)
             u[5 * (k - 1) + a] = acc;
         }
 }
+/* the solve's objective carries IPOPT's scaling factor P->df (1 unless the starting point's gradient exceeds 100) */
 static double pobj(const oprob* P, const double* pv)
 {
-    if (P->dd) return dd_objective(P, pv);
+    if (P->dd) return P->df * dd_objective(P, pv);
     double u[OMAXV];
     u_of_p(P, pv, u);
-    return oracle_objective(P, u);
+    return P->df * oracle_objective(P, u);
 }
 static void pcons(const oprob* P, const double* pv, double* c)
 {
@@ -937,6 +941,7 @@ static void pgrad(const oprob* P, const double* pv, double* gp)
 {
     if (P->dd) {
         dd_gradient(P, pv, gp);
+        for (int j = 0; j < P->n; ++j) gp[j] *= P->df;
         return;
     }
     double u[OMAXV], gu[OMAXV];
@@ -946,7 +951,7 @@ static void pgrad(const oprob* P, const double* pv, double* gp)
     for (int j = 0; j < np_; ++j) {
         double acc = 0;
         for (int i = 0; i < nu; ++i) acc += P->K->U[i][j] * gu[i];
-        gp[j] = acc;
+        gp[j] = P->df * acc;
     }
 }
 static void pjac(const oprob* P, const double* pv, double* Jp)
@@ -967,10 +972,14 @@ static void pjac(const oprob* P, const double* pv, double* Jp)
             Jp[r * np_ + j] = acc;
         }
 }
-static void phess(const oprob* P, const double* pv, const double* y, double* Hp)
+/* Hessian of L = df f - y^T c = df (f - (y / df)^T c) */
+static void phess(const oprob* P, const double* pv, const double* y_, double* Hp)
 {
+    double y[OMAXM];
+    for (int i = 0; i < P->m; ++i) y[i] = y_[i] / P->df;
     if (P->dd) {
         dd_hessian(P, pv, y, Hp);
+        for (int i = 0; i < P->n * P->n; ++i) Hp[i] *= P->df;
         return;
     }
     double u[OMAXV], Hu[OMAXV * OMAXV], T[OMAXV * 3 * OMAXN];
@@ -987,8 +996,25 @@ static void phess(const oprob* P, const double* pv, const double* y, double* Hp)
         for (int b = 0; b < np_; ++b) {
             double acc = 0;
             for (int i = 0; i < nu; ++i) acc += P->K->U[i][a] * T[i * np_ + b];
-            Hp[a * np_ + b] = acc;
+            Hp[a * np_ + b] = P->df * acc;
         }
+}
+
+/* IPOPT's default NLP scaling (nlp_scaling_method = gradient-based, nlp_scaling_max_gradient = 100,
+   nlp_scaling_min_value = 1e-8), evaluated at the user's starting point u0 in the reference's own variables: the
+   objective is scaled by 100 / max|grad f(u0)| where that maximum exceeds 100.  Constraint rows would be scaled the
+   same way, but their gradients stay below 2 in u for these NLPs (tests/test_oracle.py), so every
+   dc_i is 1. */
+static double obj_scaling(const oprob* P, const double* u0)
+{
+    double g[OMAXV];
+    if (P->dd)
+        dd_gradient(P, u0, g);
+    else
+        gradient(P, u0, g);
+    double gm = 0.0;
+    for (int i = 0; i < P->n; ++i) gm = fmax(gm, fabs(g[i]));
+    return gm > 100.0 ? fmax(1e-8, 100.0 / gm) : 1.0;
 }
 
 #define REST_FAIL 6
@@ -1042,6 +1068,7 @@ static void osolve(oprob* P, const double* u0, double* uout, osolve_info* info)
         for (int k = 0; k < P->N; ++k)
             for (int c = 0; c < 3; ++c) u[3 * k + c] = Pp0[k][c];
     }
+    P->df = obj_scaling(P, u0);
     double mu = cfg->mu_init;
     double c[OMAXM], s[OMAXM], zl[OMAXM], zu[OMAXM];
     pcons(P, u, c);

@@ -420,3 +420,56 @@ def test_goal_singular_abort_semantics(coracle, variant):
     r0, pu0 = res[0]
     assert r0["status"][0] != -13 and r0["iters"][0] > 0 and np.isfinite(r0["u"]).all()
     assert np.abs(r0["u"][0] - pu0).max() <= 1e-6
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2])
+def test_nlp_scaling_semantics(coracle, variant):
+    """IPOPT's default NLP scaling (nlp_scaling_method = gradient-based, nlp_scaling_max_gradient = 100; the reference
+    sets no scaling option, MPC_LIP_modi.py:284-290, MPC_DD_sig_step.py:181-189): at the starting point, the objective is
+    scaled by df = 100 / max|grad f(u0)| (the gradient in the reference's u) where that exceeds 100.  An instance started
+    near the goal facing away from it (heading error ~2.5 rad: gradient > 100): both oracles scale, agree, and solve
+    the same NLP as the unscaled oracle with weights q, p, r (and DD's smoothness weight) times df — the objective is
+    linear in them.  Constraint gradients stay far below 100 in u, so no row is scaled (dc = 1, as both oracles assume)."""
+    dd = variant == 2
+    N = 3
+    goal = np.array([5.0, 5.0])
+    cir = np.array([[7.0, 4.0, 0.4], [3.0, 6.5, 0.3]])
+    if dd:
+        x0 = np.array([4.7, 4.8, np.pi + 0.9])
+        last_u = np.array([0.5, 0.0])
+        u0 = np.tile(last_u, N)
+        o = O.default_cfg(variant, N, nc_max=2, ne_max=0)
+        pr = O.DDProblem(o, x0, goal, cir, np.zeros((0, 5)), last_u, split=True)
+        sp = O.ScaledProblem(pr, u0)
+    else:
+        x0 = np.array([4.7, 4.8, -0.3, -0.1, np.pi + 0.9])
+        u0 = np.tile(x0, N)
+        o = O.default_cfg(variant, N, nc_max=2, ne_max=0)
+        pr = O.Problem(o, x0, goal, 1, cir, np.zeros((0, 5)))
+        fp = O.FootholdProblem(pr.split_copy())
+        sp = O.ScaledProblem(fp, fp.p_of_u(u0))
+    df = sp.df
+    assert 0.0 < df < 1.0, df
+    assert sp.max_constraint_gradient < 10.0, sp.max_constraint_gradient
+    c = coracle.default_cfg(variant, N, nc_max=2, ne_max=0)
+    if dd:
+        r = coracle.solve_batch_dd(c, x0[None], goal[None], cir[None], np.array([2], np.int32), None, None, u0[None],
+                                   last_u[None])
+        pu, pst, pit = O.dd_solve(O.DDProblem(o, x0, goal, cir, np.zeros((0, 5)), last_u), u0)
+    else:
+        r = coracle.solve_batch(c, x0[None], goal[None], np.ones(1, np.int8), cir[None], np.array([2], np.int32), None,
+                                None, u0[None])
+        pu, pst, pit = O.solve_footholds(pr, u0)
+    assert r["status"][0] == pst and r["iters"][0] == pit
+    assert np.abs(r["u"][0] - pu).max() <= 1e-9
+    # the same NLP with the objective's weights scaled by df, solved without scaling (its gradient is then 100)
+    kw = dict(q=o.q * df, p=o.p * df, r=o.r * df) | (dict(dd_t=o.dd_t * df) if dd else {})
+    cs = coracle.default_cfg(variant, N, nc_max=2, ne_max=0, **kw)
+    if dd:
+        rs = coracle.solve_batch_dd(cs, x0[None], goal[None], cir[None], np.array([2], np.int32), None, None,
+                                    u0[None], last_u[None])
+    else:
+        rs = coracle.solve_batch(cs, x0[None], goal[None], np.ones(1, np.int8), cir[None], np.array([2], np.int32),
+                                 None, None, u0[None])
+    assert rs["status"][0] == r["status"][0] and abs(int(rs["iters"][0]) - int(r["iters"][0])) <= 1
+    assert np.abs(rs["u"][0] - r["u"][0]).max() <= 1e-6
