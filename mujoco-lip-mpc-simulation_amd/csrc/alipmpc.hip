@@ -1648,7 +1648,9 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* wsb, int wv, lo
                 break;
             }
             if (it >= it_end) break;
-            const R mu_min = w.cst[K_TOL] / R(10.0);
+            // IPOPT's floor min(tol, compl_inf_tol) / (barrier_tol_factor + 1 = 11) (MonotoneMuUpdate): tol / 11 for
+            // every tol <= compl_inf_tol = 1e-4 (the fp32 defaults above it keep their own tol / 11)
+            const R mu_min = w.cst[K_TOL] / R(11.0);
             const R mu_prev = mu;
             for (int t = 0; t < 8; ++t) {
                 const R cm = anyw ? fmax(fabs(whi - mu), fabs(wlo - mu)) : R(0.0);
@@ -3593,7 +3595,7 @@ __global__ __launch_bounds__(256, dd_solve_waves<RPL>()) void dd_solve_kernel(KP
         }
         if (it == max_iter) break;
         {
-            const double mu_min = w.cst[DK_TOL] / 10.0;
+            const double mu_min = w.cst[DK_TOL] / 11.0;   // (IPOPT's floor, as solve_kernel)
             const double mu_prev = mu;
             for (int t = 0; t < 8; ++t) {
                 double cm = 0.0;

@@ -1133,7 +1133,9 @@ static void osolve(oprob* P, const double* u0, double* uout, osolve_info* info)
             break;
         }
         if (it == cfg->max_iter) break;
-        double mu_min = cfg->tol / 10.0, mu_old = mu;
+        /* IPOPT's floor min(tol, compl_inf_tol) / (barrier_tol_factor + 1 = 11) (MonotoneMuUpdate): tol / 11 for
+           tol <= compl_inf_tol = 1e-4 (the fp32 programs' larger tolerances keep tol / 11) */
+        double mu_min = cfg->tol / 11.0, mu_old = mu;
         for (int t = 0; t < 8; ++t) {
             if (ERR(mu) <= 10.0 * mu && mu > mu_min)
                 mu = fmax(mu_min, fmin(0.2 * mu, mu * sqrt(mu)));
