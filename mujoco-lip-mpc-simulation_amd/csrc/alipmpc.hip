@@ -1795,7 +1795,7 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* wsb, int wv, lo
                         fill(dw);
                         if (gj_regs<n>(a, lane)) break;
                         dw *= dw_last == R(0.0) ? R(100.0) : R(8.0);
-                        if (dw > R(sizeof(R) == 8 ? 1e40 : 1e30)) {
+                        if (dw > R(sizeof(R) == 8 ? 1e40 : 1e30)) {   // (not IPOPT's 1e20)
                             fact_ok = false;
                             break;
                         }
@@ -1817,7 +1817,7 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* wsb, int wv, lo
                         wave_sync();
                         if (gj_lds<n, GJLD>(w.S, lane)) break;
                         dw *= dw_last == R(0.0) ? R(100.0) : R(8.0);
-                        if (dw > R(sizeof(R) == 8 ? 1e40 : 1e30)) {
+                        if (dw > R(sizeof(R) == 8 ? 1e40 : 1e30)) {   // (not IPOPT's 1e20)
                             fact_ok = false;
                             break;
                         }
@@ -1839,7 +1839,7 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* wsb, int wv, lo
                                    (lane == j ? dw : R(0.0));
                         if (chol_rows<n>(a, myidg, lane)) break;
                         dw *= dw_last == R(0.0) ? R(100.0) : R(8.0);
-                        if (dw > R(sizeof(R) == 8 ? 1e40 : 1e30)) {
+                        if (dw > R(sizeof(R) == 8 ? 1e40 : 1e30)) {   // (not IPOPT's 1e20)
                             fact_ok = false;
                             break;
                         }
@@ -3676,7 +3676,7 @@ __global__ __launch_bounds__(256, dd_solve_waves<RPL>()) void dd_solve_kernel(KP
                         a[j] = (lane < n ? w.K[lane * KLD + j] : (lane == j ? 1.0 : 0.0)) + (lane == j ? dw : 0.0);
                     if (chol_rows<n>(a, myidg, lane)) break;
                     dw *= dw_last == 0.0 ? 100.0 : 8.0;
-                    if (dw > 1e40) {
+                    if (dw > 1e40) {   // (not IPOPT's 1e20)
                         fact_ok = false;
                         break;
                     }

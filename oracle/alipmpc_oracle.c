@@ -1170,7 +1170,7 @@ static void osolve(oprob* P, const double* u0, double* uout, osolve_info* info)
                 for (int a = 0; a < n; ++a) L[a * n + a] += dw;
                 if (chol(L, n)) break;
                 dw *= dw_last == 0 ? 100.0 : 8.0;
-                if (dw > 1e40) {
+                if (dw > 1e40) {   /* (not IPOPT's max_hessian_perturbation 1e20: DESIGN.md §2) */
                     fact_ok = 0;
                     break;
                 }
