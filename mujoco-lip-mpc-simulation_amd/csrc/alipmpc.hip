@@ -1172,6 +1172,75 @@ __device__ void hess_blocks(const WSS<N, R>& w, int lane, int rps, int nobs, int
     S[5 * 8 + 5] = h55; S[6 * 8 + 6] = h55;
 }
 
+// sum over each 16-lane DPP row (every lane of the row receives its row's sum)
+template <class T>
+__device__ __forceinline__ T rsum16(T v)
+{
+    v += dpp<0xB1>(v);
+    v += dpp<0x4E>(v);
+    v += dpp<0x141>(v);
+    v += dpp<0x140>(v);
+    return v;
+}
+
+// hess_blocks with the obstacle terms spread over lanes (16 (N + 1) <= 64 lanes): lane 16 kb + j takes
+// obstacle slots j and j + 16's terms on block kb — the post-step state of step kb - 1 and the pre-step state of step kb, whose
+// multipliers combine as y_post + gamma_1 y_pre on the same form — and each block's sum is one 16-lane DPP reduction.
+// The serial form above walks the slots with one dependent LDS round trip per unrolled group: on a lone wave that
+// phase had cost 3.2 k of the 22 k cycles of an iteration (tools/stamps.py, profiles/r5).  The same terms, summed in
+// another order (rounding-level differences only).
+template <int N, class R>
+__device__ void hess_blocks_lanes(const WSS<N, R>& w, int lane, int rps, int nobs, int modi)
+{
+    static_assert(16 * (N + 1) <= WAVE, "one 16-lane row per block");
+    const int kb = lane >> 4, j = lane & 15;
+    const R gm1 = w.cst[K_GM1];
+    R t00 = R(0), t01 = R(0), t11 = R(0);
+    // slots j and j + 16 (ALIPMPC_MAX_OBS = 24); inactive slots have y = 0 and a zero form
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int js = j + 16 * h;
+        if (kb >= 1 && kb <= N && js < nobs) {
+            const R* o = w.obs6 + 6 * js;
+            R y = w.ry[(kb - 1) * rps + 2 + js];
+            if (kb < N) y = fma(w.ry[kb * rps + 2 + js], gm1, y);
+            t00 = fma(R(-2) * y, o[2], t00);
+            t01 = fma(-y, o[3], t01);
+            t11 = fma(R(-2) * y, o[4], t11);
+        }
+    }
+    const R a00 = rsum16(t00), a01 = rsum16(t01), a11 = rsum16(t11);
+    if (j != 0 || kb > N) return;
+    R h00 = 0, h01 = 0, h11 = 0, h04 = 0, h14 = 0, h44 = 0, h24 = 0, h34 = 0;
+    R h05 = 0, h55 = 0;
+    if (kb >= 1) {
+        const R* ho = w.hobj + 6 * kb;
+        h00 = ho[0] + a00; h01 = ho[1] + a01; h11 = ho[2] + a11; h04 = ho[3]; h14 = ho[4]; h44 = ho[5];
+        const int base = (kb - 1) * rps;
+        const R ct = w.CT[kb], st = w.ST[kb];
+        const R vx = w.V[gx(kb, 2)], vy = w.V[gx(kb, 3)];
+        const R vbx = ct * vx + st * vy, vby = -st * vx + ct * vy;
+        const R wbx = w.ry[base + 0] + (modi ? w.ry[base + rps - 2] + w.ry[base + rps - 1] : R(0));
+        const R wby = w.ry[base + 1];
+        h24 = wbx * st + wby * ct;
+        h34 = -wbx * ct + wby * st;
+        h44 += wbx * vbx + wby * vby;
+    }
+    if (kb < N) {
+        const R yl = w.ry[kb * rps + 2 + nobs];
+        h00 -= 2 * yl;
+        h11 -= 2 * yl;
+        h05 = 2 * yl;
+        h55 = -2 * yl;
+    }
+    R* S = w.S + 64 * kb;
+    S[0 * 8 + 0] = h00; S[0 * 8 + 1] = h01; S[1 * 8 + 0] = h01; S[1 * 8 + 1] = h11;
+    S[0 * 8 + 4] = h04; S[4 * 8 + 0] = h04; S[1 * 8 + 4] = h14; S[4 * 8 + 1] = h14;
+    S[2 * 8 + 4] = h24; S[4 * 8 + 2] = h24; S[3 * 8 + 4] = h34; S[4 * 8 + 3] = h34; S[4 * 8 + 4] = h44;
+    S[0 * 8 + 5] = h05; S[5 * 8 + 0] = h05; S[1 * 8 + 6] = h05; S[6 * 8 + 1] = h05;
+    S[5 * 8 + 5] = h55; S[6 * 8 + 6] = h55;
+}
+
 // ------------------------------------------------------------------------------------------------
 // the solve kernel: one instance per wave.
 //   Row layout (lane r = row r [+ 64]): values, multipliers, slacks, bound terms, and a REGISTER copy of
@@ -1369,6 +1438,9 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* wsb, int wv, lo
     // reference's u through Gu (d x_k / d u), and the objective scaled by 100 / max |grad f| where that exceeds 100 —
     // the objective is linear in its weights, so the weights are scaled (constraint rows' gradients stay below 4 in u:
     // no row scaling)
+#ifdef ALIP_SCAL_P1_ONLY   // dev A/B timing only
+    if (rec < 0)
+#endif
     {
 #pragma unroll
         for (int q = 0; q < RPL; ++q) {
@@ -1392,7 +1464,11 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* wsb, int wv, lo
             }
         }
         const R gm = wmax(fabs(gu));
+#ifdef ALIP_NO_OBJ_SCALING   // dev A/B timing only (changes the algorithm where the gradient exceeds 100)
+        const R dfo = R(1);
+#else
         const R dfo = uni(gm > R(100) ? fmax(R(1e-8), R(100) / gm) : R(1));
+#endif
         wave_sync();
         if (dfo != R(1)) {
             if (lane == 0) {
@@ -1682,7 +1758,12 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* wsb, int wv, lo
             }
         }
         RELANE();
-        hess_blocks<N, R>(w, lane, rps, nobs, modi);
+#ifndef ALIP_HESS_SERIAL
+        if constexpr (16 * (N + 1) <= WAVE)
+            hess_blocks_lanes<N, R>(w, lane, rps, nobs, modi);
+        else
+#endif
+            hess_blocks<N, R>(w, lane, rps, nobs, modi);
         wave_sync();
         STAMP(3);
         // ---- K = J^T Sigma J + G^T S G by f64 MFMA (two accumulator chains), rhs = J^T w - grad f
@@ -1736,7 +1817,11 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* wsb, int wv, lo
                 // S rows 0..3 (even s: t & 7 = g4) have nonzeros in columns {0, 1, 4, 5, 6} only, rows 4..7 in {0..6}
                 // (hess_blocks' pattern; the rest of S stays zero): the zero products are skipped (+0 terms, the same
                 // sums)
+#ifdef ALIP_S_DENSE   // dev A/B: every column
+                const unsigned SCOLS = 0xFFu;
+#else
                 const unsigned SCOLS = (s & 1) ? 0x7Fu : 0x73u;   // (s is unrolled: a constant per step)
+#endif
 #pragma unroll
                 for (int T = 0; T < NT; ++T) {
                     gv[T] = G[t * NCP + 16 * T + col];

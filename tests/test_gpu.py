@@ -1092,12 +1092,10 @@ def test_closed_loop_step_failures_vs_oracle(gpu_lib, coracle, program, prec):
     _artifact(f"closed_loop_m3_{program}_{prec}.json", {"episodes": B, "ticks": int((o["status"] != -10).sum()),
                                                         "gpu": cnt(o["status"]), "oracle": cnt(ref["status"]),
                                                         "oracle_same_tol": cnt(same["status"])})
-    # (fp32, r5: -3 on ~0.03 % of the ticks where the oracle's loop has none — warm starts whose plan sits within 2e-15 of
-    # the goal, where the exact Hessian of the heading term is ~1e54 after IPOPT's scaling floor df = 1e-8 and no
-    # regularisation up to 1e40 makes the KKT matrix positive definite; on those same inputs the oracle does not converge
-    # either (-1 at the iteration cap, tools/cl_m3.py: profiles/r5/m3).  The bound is 0.05 % of the ticks.)
-    allow = 0 if not prec else int(0.0005 * (o["status"] != -10).sum())
-    assert (o["status"] == -3).sum() <= (same["status"] == -3).sum() + allow, (cnt(o["status"]), cnt(same["status"]))
+    # (fp32, r5: the goal-frame fp32 lane build had logged -3 on 0.03 % of the ticks — iterates converging onto the goal,
+    # where a goal-frame |g - p| kept shrinking to ~1e-150 and the heading term's curvature 1 / |g - p|^4 overflowed the
+    # KKT matrix; the objective's goal differences are now taken in map coordinates, as the oracle rounds them: none)
+    assert (o["status"] == -3).sum() <= (same["status"] == -3).sum(), (cnt(o["status"]), cnt(same["status"]))
     # iteration-cap stops and converged ticks as the same-tolerance oracle's (r4's fp32 loop: 3x the cap stops, 74 %
     # vs 91 % converged — the fp32 heading error near the goal)
     ran = o["status"] != -10
