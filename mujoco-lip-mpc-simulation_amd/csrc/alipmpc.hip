@@ -1438,9 +1438,6 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* wsb, int wv, lo
     // reference's u through Gu (d x_k / d u), and the objective scaled by 100 / max |grad f| where that exceeds 100 —
     // the objective is linear in its weights, so the weights are scaled (constraint rows' gradients stay below 4 in u:
     // no row scaling)
-#ifdef ALIP_SCAL_P1_ONLY   // dev A/B timing only
-    if (rec < 0)
-#endif
     {
 #pragma unroll
         for (int q = 0; q < RPL; ++q) {
