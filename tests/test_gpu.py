@@ -203,8 +203,9 @@ def test_solve_cfg2_batch_vs_oracle(gpu_lib, coracle):
     assert np.allclose(o["u"].reshape(-1, 3, 5), o["x_pred"], rtol=0, atol=0)
 
 
+# (N <= 3 with more than 16 obstacle slots: the Hessian blocks' second slot per lane, hess_blocks_lanes)
 @pytest.mark.parametrize("variant,N,n_cir,n_elp", [(1, 3, 4, 0), (0, 3, 3, 3), (0, 5, 5, 5), (0, 1, 2, 0),
-                                                   (0, 4, 5, 0), (0, 6, 3, 0)])
+                                                   (0, 4, 5, 0), (0, 6, 3, 0), (0, 3, 12, 8), (1, 2, 14, 6)])
 def test_solve_variants_vs_oracle(gpu_lib, coracle, variant, N, n_cir, n_elp):
     from alipmpc import scenes
     bt = scenes.make_batch(256, seed=100 + N + n_elp, n_cir=n_cir, n_elp=n_elp, N=N)
