@@ -124,11 +124,12 @@ constexpr int FAIL_GOAL = 1 << 16;   // solve_kernel's fail_it tag of a cfg.goal
 constexpr int CKPT_ROW = 12;
 __host__ __device__ constexpr int ckpt_doubles(int rpl) { return WAVE * (CKPT_ROW * rpl + 5) + 16; }
 #ifndef ALIP_SPLIT_IT
-#define ALIP_SPLIT_IT 16
+#define ALIP_SPLIT_IT 14   // (r5 sweep on cfg2: 12 / 13 / 14 / 15 / 16 / 18 / 20 = 0.58 / 0.59 / 0.537 / 0.55 / 0.543 / 0.545 / 0.55 ms)
 #endif
 constexpr int SPLIT_IT_DEFAULT = ALIP_SPLIT_IT;   // phase-1 iteration cap of the split launch (launch_solve)
 constexpr int SPLIT_TR_DEFAULT = 0;               // phase-1 trial cut of a cold solve (0 = off: no team records)
-constexpr int CL_SPLIT_IT_DEFAULT = 16;           // the closed loop's per-tick solves: phase-1 cap
+constexpr int CL_SPLIT_IT_DEFAULT = 20;           // the closed loop's per-tick solves: phase-1 cap (r5: 16 / 18 / 20 / 22 /
+                                                   // 24 = 23.7 / 22.95 / 22.7 / 22.8 / 23.6 ms per loop)
 constexpr int CL_SPLIT_TR_DEFAULT = 40;           // and trial cut
 constexpr int CL_GROUPS_DEFAULT = 2;              // closed loop: episode groups on streams of their own (4: host-bound)
 static int env_groups()
