@@ -4657,7 +4657,9 @@ void launch_solve(const KP& P0, size_t smem, hipStream_t st, unsigned* res_out)
 #ifdef ALIP_DEV_ONLY_KSM   // dev builds for register reports (tools/regs.py): one row-step count only
     ALIP_GO(ALIP_DEV_ONLY_KSM);
 #else
-    if (P0.mo4 <= 32)
+    if (P0.mo4 <= 16)   // (r5: sig_step / modi with no obstacle slots at N <= 3, cfg1: 0.1255 -> 0.1195 ms)
+        ALIP_GO(4);
+    else if (P0.mo4 <= 32)
         ALIP_GO(8);
     else if (P0.mo4 <= 40)
         ALIP_GO(10);
@@ -5170,7 +5172,7 @@ KP make_kp(const Handle* h, long long B, bool solve)
 // J-layout steps (4 rows each) of the compiled solve kernels; mo4 is rounded up to 4 * ksm_of(rows)
 int ksm_of(int rows)
 {
-    static const int K[] = {8, 10, 12, 16, 24, 32, 48};
+    static const int K[] = {4, 8, 10, 12, 16, 24, 32, 48};
     for (int k : K)
         if (rows <= 4 * k) return k;
     return 1 << 20;
