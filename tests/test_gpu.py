@@ -203,14 +203,18 @@ def test_solve_cfg2_batch_vs_oracle(gpu_lib, coracle):
     assert np.allclose(o["u"].reshape(-1, 3, 5), o["x_pred"], rtol=0, atol=0)
 
 
-# (N <= 3 with more than 16 obstacle slots: the Hessian blocks' second slot per lane, hess_blocks_lanes)
+# (N <= 3 with more than 16 obstacle slots: the Hessian blocks' second slot per lane, hess_blocks_lanes; no obstacle
+# slots at N <= 3: the 4-row-step J layout, solve_kernel<N, 4, ...>)
 @pytest.mark.parametrize("variant,N,n_cir,n_elp", [(1, 3, 4, 0), (0, 3, 3, 3), (0, 5, 5, 5), (0, 1, 2, 0),
-                                                   (0, 4, 5, 0), (0, 6, 3, 0), (0, 3, 12, 8), (1, 2, 14, 6)])
+                                                   (0, 4, 5, 0), (0, 6, 3, 0), (0, 3, 12, 8), (1, 2, 14, 6),
+                                                   (1, 3, 0, 0), (0, 2, 0, 0)])
 def test_solve_variants_vs_oracle(gpu_lib, coracle, variant, N, n_cir, n_elp):
     from alipmpc import scenes
     bt = scenes.make_batch(256, seed=100 + N + n_elp, n_cir=n_cir, n_elp=n_elp, N=N)
     cfg = gpu_lib.default_cfg(variant, N, nc_max=n_cir, ne_max=n_elp)
     s = gpu_lib.Solver(cfg)
+    if n_cir + n_elp == 0:
+        assert s.solve_program().startswith(f"solve_kernel<{N},4,"), s.solve_program()
     o = s.solve(bt["x0"], bt["goal"], bt["leg"], bt["cir"], bt["nc"], bt["elp"], bt["ne"], u0=bt["u0"])
     ref = _oracle_solve(coracle, dict(variant=variant, N=N, nc_max=n_cir, ne_max=n_elp), bt)
     _compare(o, ref, min_conv=0.5, min_agree=0.95, min_status=0.9)
