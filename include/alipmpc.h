@@ -132,10 +132,23 @@ typedef struct alipmpc_cfg {
                            ends the solve with status ALIPMPC_INVALID_NUMBER_DETECTED (-13) at the first iterate
                            (starting point or accepted step) with such a state, and that iterate is returned.
                            (Fills the struct's tail padding: sizeof(alipmpc_cfg) is unchanged.) */
+    int32_t restoration;   /* what follows a failed filter line search (IPOPT's default path; no reference option
+                           selects it): ALIPMPC_RESTORATION_IPOPT (0, default) — IPOPT's feasibility restoration phase:
+                           the l1 feasibility problem min rho sum(p + n) + zeta/2 |D_R (x - x_R)|^2 s.t. c(x) - s - p + n
+                           = 0 (rho = 1000, zeta = sqrt(mu)) solved by the same interior point until an iterate the
+                           original filter accepts with 0.9 of the violation, status 2 (Infeasible_Problem_Detected)
+                           only when it converges to a point of local infeasibility;
+                           ALIPMPC_RESTORATION_SUBSTITUTE (1) — the rounds-1..5 substitute: the shortest trial step,
+                           slacks reset onto c(u), filter reset, status 2 after 6 such events.  The DD variant always
+                           runs the substitute. */
+    int32_t reserved_;  /* zero */
 } alipmpc_cfg;
 
 #define ALIPMPC_GOAL_SINGULAR_ZERO 0
 #define ALIPMPC_GOAL_SINGULAR_ABORT 1
+
+#define ALIPMPC_RESTORATION_IPOPT 0
+#define ALIPMPC_RESTORATION_SUBSTITUTE 1
 
 /* Fill *out with the reference's constants for a variant and horizon.  nc_max = ne_max = 6, precision
  * fp64, max_iter = the reference's IPOPT cap (modi 30, sig_step 20, DD 40). */

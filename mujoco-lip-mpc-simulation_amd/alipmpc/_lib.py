@@ -34,7 +34,8 @@ class Cfg(ctypes.Structure):
                [(k, ctypes.c_double) for k in
                 ("tol", "acceptable_tol", "dt", "H", "g", "leg2_max", "bvx_lo", "bvx_hi", "bvy_lo", "bvy_hi",
                  "dtheta_max", "q", "p", "r", "gamma", "s", "detect_r2", "dd_t", "mu_init")] + \
-               [("program", ctypes.c_int32), ("goal_singular", ctypes.c_int32)]
+               [("program", ctypes.c_int32), ("goal_singular", ctypes.c_int32), ("restoration", ctypes.c_int32),
+                ("reserved_", ctypes.c_int32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

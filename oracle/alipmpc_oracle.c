@@ -456,8 +456,8 @@ static void jacobian(const oprob* P, const double* u, double* J /* m x n */)
     }
 }
 
-/* exact Hessian of L = f - y^T c */
-static void hessian(const oprob* P, const double* u, const double* y, double* H /* n x n */)
+/* exact Hessian of L = of f - y^T c (of = 0: the restoration phase's constraint part) */
+static void hessian_of(const oprob* P, const double* u, const double* y, double of, double* H /* n x n */)
 {
     const alipmpc_cfg* c = P->cfg;
     const oconsts* K = P->K;
@@ -467,7 +467,7 @@ static void hessian(const oprob* P, const double* u, const double* y, double* H 
     double Hl[OMAXN + 1][5][5];
     memset(Hl, 0, sizeof(Hl));
     for (int i = 0; i < n * n; ++i) H[i] = 0;
-    for (int k = 1; k <= N; ++k) {
+    for (int k = 1; k <= N && of != 0.0; ++k) {
         double w = c->q + (k == 1 ? c->p : 0.0);
         Hl[k][0][0] += 2 * w;
         Hl[k][1][1] += 2 * w;
@@ -558,6 +558,7 @@ static void hessian(const oprob* P, const double* u, const double* y, double* H 
             }
     }
 }
+static void hessian(const oprob* P, const double* u, const double* y, double* H) { hessian_of(P, u, y, 1.0, H); }
 
 /* ------------------------------------------------------------------------------------------------ */
 static int chol(double* A, int n)
@@ -972,8 +973,8 @@ static void pjac(const oprob* P, const double* pv, double* Jp)
             Jp[r * np_ + j] = acc;
         }
 }
-/* Hessian of L = df f - y^T c = df (f - (y / df)^T c) */
-static void phess(const oprob* P, const double* pv, const double* y_, double* Hp)
+/* Hessian of L = of df f - y^T c = df (of f - (y / df)^T c) */
+static void phess_of(const oprob* P, const double* pv, const double* y_, double of, double* Hp)
 {
     double y[OMAXM];
     for (int i = 0; i < P->m; ++i) y[i] = y_[i] / P->df;
@@ -984,7 +985,7 @@ static void phess(const oprob* P, const double* pv, const double* y_, double* Hp
     }
     double u[OMAXV], Hu[OMAXV * OMAXV], T[OMAXV * 3 * OMAXN];
     u_of_p(P, pv, u);
-    hessian(P, u, y, Hu);
+    hessian_of(P, u, y, of, Hu);
     const int nu = 5 * P->N, np_ = 3 * P->N;
     for (int i = 0; i < nu; ++i)
         for (int j = 0; j < np_; ++j) {
@@ -999,6 +1000,7 @@ static void phess(const oprob* P, const double* pv, const double* y_, double* Hp
             Hp[a * np_ + b] = P->df * acc;
         }
 }
+static void phess(const oprob* P, const double* pv, const double* y_, double* Hp) { phess_of(P, pv, y_, 1.0, Hp); }
 
 /* IPOPT's default NLP scaling (nlp_scaling_method = gradient-based, nlp_scaling_max_gradient = 100,
    nlp_scaling_min_value = 1e-8), evaluated at the user's starting point u0 in the reference's own variables: the
@@ -1042,6 +1044,338 @@ static int at_goal(const oprob* P, const double* pv)
         if (dxg * dxg + dyg * dyg == 0.0) return 1;
     }
     return 0;
+}
+
+/* IPOPT's feasibility restoration phase (Wächter & Biegler 2006 §3.3; IPOPT's MinC_1NrmRestorationPhase, published
+   defaults, version unpinned); mirrors np_oracle._resto (proximity on the footholds, D_R = 1 / max(1, |p_R|)):
+     min rho sum(p + n) + zeta/2 sum_j D_j^2 (x_j - xR_j)^2  s.t.  c(x) - p + n - s = 0, cl <= s <= cu, p, n >= 0
+   rho = 1000, zeta = sqrt(mu_R), mu_R from max(mu, |c - s|_inf); p, n from IPOPT eq. (33); y = 0; slack multipliers
+   min(rho, current).  Returns RS_OK (back to the regular phase: x, s, zl, zu updated), RS_INFEASIBLE (restoration
+   converged with the violation above 1e-4: Infeasible_Problem_Detected), RS_MAXITER, RS_FAILED; *it advances by the
+   restoration's iterations. */
+enum { RS_OK = 0, RS_INFEASIBLE = 1, RS_MAXITER = 2, RS_FAILED = 3 };
+#define RESTO_RHO 1000.0
+#define RESTO_KAPPA 0.9
+#define RESTO_VIOL_TOL 1e-4
+#define RESTO_MULT_RESET 1000.0
+
+static double ftb(double v, double dv, double tau, double a) { return dv < 0 ? fmin(a, -tau * v / dv) : a; }
+
+static int oresto(oprob* P, double* x, double* s, double* zl, double* zu, double mu_o, const double* cl,
+                  const double* cu, const int* hl, const int* hu, const double* fo, int nfo, double theta_R, int* it,
+                  int max_iter, double tol)
+{
+    const int n = 3 * P->N, m = P->m;
+    const double rho = RESTO_RHO;
+    double xR[OMAXV], d2[OMAXV], c[OMAXM], pp[OMAXM], nn[OMAXM], zp[OMAXM], zn[OMAXM], vl[OMAXM], vu[OMAXM];
+    double y[OMAXM], s0[OMAXM], J[OMAXM * OMAXV], H[OMAXV * OMAXV], Kmat[OMAXV * OMAXV], L[OMAXV * OMAXV];
+    double rhs[OMAXV], gx[OMAXV], dx[OMAXV], dl[OMAXM], du[OMAXM], D[OMAXM], b[OMAXM], dy[OMAXM], dp[OMAXM];
+    double dn[OMAXM], ds[OMAXM], dzp[OMAXM], dzn[OMAXM], dvl[OMAXM], dvu[OMAXM], Sp[OMAXM], Sn[OMAXM], Ss[OMAXM];
+    double xt[OMAXV], pt[OMAXM], nt[OMAXM], st[OMAXM], ct[OMAXM];
+    static const double gth = 1e-5, gph = 1e-8, sth = 1.1, sph = 2.3, eta = 1e-8, gal = 0.05;
+    memcpy(xR, x, sizeof(double) * n);
+    for (int j = 0; j < n; ++j) {
+        double dd = 1.0 / fmax(1.0, fabs(xR[j]));
+        d2[j] = dd * dd;
+    }
+    pcons(P, x, c);
+    double mu = mu_o;
+    for (int i = 0; i < m; ++i) mu = fmax(mu, fabs(c[i] - s[i]));
+    for (int i = 0; i < m; ++i) {
+        double r = c[i] - s[i], a = (mu - rho * r) / (2 * rho);
+        double sq = sqrt(a * a + mu * r / (2 * rho));
+        nn[i] = a >= 0 ? a + sq : (mu * r / (2 * rho)) / (sq - a);
+        pp[i] = r + nn[i];
+        zp[i] = mu / pp[i];
+        zn[i] = mu / nn[i];
+        vl[i] = hl[i] ? fmin(rho, zl[i]) : 0.0;
+        vu[i] = hu[i] ? fmin(rho, zu[i]) : 0.0;
+        y[i] = 0.0;
+        s0[i] = s[i];
+    }
+    const int maxf = max_iter + 2;
+    double* ft = (double*)malloc(sizeof(double) * 2 * maxf);
+    int nf = 0;
+    double th0 = 0;
+    for (int i = 0; i < m; ++i) th0 += fabs(c[i] - pp[i] + nn[i] - s[i]);
+    const double theta_max = 1e4 * fmax(1.0, th0), theta_min = 1e-4 * fmax(1.0, th0);
+    double dw_last = 0.0;
+    int first = 1, nb = 2 * m, ret;
+    for (int i = 0; i < m; ++i) nb += hl[i] + hu[i];
+    const int nvar = n + 2 * m;
+    for (;;) {
+        pcons(P, x, c);
+        if (!first) {
+            double th_o = 0;
+            for (int i = 0; i < m; ++i) th_o += fabs(c[i] - s[i]);
+            double ph_o = barrier(pobj(P, x), s, cl, cu, m, mu_o);
+            int acc = isfinite(ph_o) && th_o <= RESTO_KAPPA * theta_R;
+            for (int q = 0; acc && q < nfo; ++q)
+                if (!(th_o < fo[2 * q] || ph_o < fo[2 * q + 1])) acc = 0;
+            if (acc) {
+                /* back to the regular phase: slack multipliers by the complementarity Newton step over the whole
+                   restoration (fraction to the boundary), reset to 1 above bound_mult_reset_threshold */
+                const double tau = fmax(0.99, 1.0 - mu_o);
+                double ad = 1.0, zmax = 0.0;
+                double dzl[OMAXM], dzu[OMAXM];
+                for (int i = 0; i < m; ++i) {
+                    dzl[i] = hl[i] ? mu_o / (s0[i] - cl[i]) - zl[i] - zl[i] / (s0[i] - cl[i]) * (s[i] - s0[i]) : 0.0;
+                    dzu[i] = hu[i] ? mu_o / (cu[i] - s0[i]) - zu[i] + zu[i] / (cu[i] - s0[i]) * (s[i] - s0[i]) : 0.0;
+                    if (hl[i]) ad = ftb(zl[i], dzl[i], tau, ad);
+                    if (hu[i]) ad = ftb(zu[i], dzu[i], tau, ad);
+                }
+                for (int i = 0; i < m; ++i) {
+                    zl[i] += ad * dzl[i];
+                    zu[i] += ad * dzu[i];
+                    zmax = fmax(zmax, fmax(zl[i], zu[i]));
+                }
+                if (zmax > RESTO_MULT_RESET)
+                    for (int i = 0; i < m; ++i) {
+                        zl[i] = hl[i] ? 1.0 : 0.0;
+                        zu[i] = hu[i] ? 1.0 : 0.0;
+                    }
+                ret = RS_OK;
+                break;
+            }
+        }
+        first = 0;
+        pjac(P, x, J);
+        double zeta = sqrt(mu);
+        double nz = 0, ny = 0;
+        for (int i = 0; i < m; ++i) {
+            dl[i] = hl[i] ? s[i] - cl[i] : 1.0;
+            du[i] = hu[i] ? cu[i] - s[i] : 1.0;
+            ny += fabs(y[i]);
+            nz += fabs(zp[i]) + fabs(zn[i]) + fabs(vl[i]) + fabs(vu[i]);
+        }
+        const double sd = fmax(100.0, (nz + ny) / (nvar + m)) / 100.0;
+        const double sc = fmax(100.0, nz / (nb > 0 ? nb : 1)) / 100.0;
+        double dual = 0, prim = 0;
+        for (int j = 0; j < n; ++j) {
+            double a = zeta * d2[j] * (x[j] - xR[j]);
+            for (int i = 0; i < m; ++i) a -= J[i * n + j] * y[i];
+            gx[j] = a;
+            dual = fmax(dual, fabs(a));
+        }
+        for (int i = 0; i < m; ++i) {
+            dual = fmax(dual, fmax(fabs(rho + y[i] - zp[i]), fabs(rho - y[i] - zn[i])));
+            dual = fmax(dual, fabs(y[i] - vl[i] + vu[i]));
+            prim = fmax(prim, fabs(c[i] - pp[i] + nn[i] - s[i]));
+        }
+#define RERR(muv)                                                                                   \
+    ({                                                                                              \
+        double cm_ = 0;                                                                             \
+        for (int i_ = 0; i_ < m; ++i_) {                                                            \
+            cm_ = fmax(cm_, fmax(fabs(pp[i_] * zp[i_] - (muv)), fabs(nn[i_] * zn[i_] - (muv))));    \
+            if (hl[i_]) cm_ = fmax(cm_, fabs(dl[i_] * vl[i_] - (muv)));                             \
+            if (hu[i_]) cm_ = fmax(cm_, fabs(du[i_] * vu[i_] - (muv)));                             \
+        }                                                                                           \
+        fmax(fmax(dual / sd, prim), cm_ / sc);                                                      \
+    })
+        if (RERR(0.0) <= tol) {
+            double viol = 0;
+            for (int i = 0; i < m; ++i) {
+                if (hl[i]) viol = fmax(viol, P->cl[i] - c[i]);
+                if (hu[i]) viol = fmax(viol, c[i] - P->cu[i]);
+            }
+            ret = viol > RESTO_VIOL_TOL ? RS_INFEASIBLE : RS_OK;
+            break;
+        }
+        if (*it >= max_iter) {
+            ret = RS_MAXITER;
+            break;
+        }
+        const double mu_min = tol / 11.0, mu_old = mu;
+        for (int t = 0; t < 8; ++t) {
+            if (RERR(mu) <= 10.0 * mu && mu > mu_min)
+                mu = fmax(mu_min, fmin(0.2 * mu, mu * sqrt(mu)));
+            else
+                break;
+        }
+#undef RERR
+        if (mu != mu_old) {
+            nf = 0;
+            zeta = sqrt(mu);
+            for (int j = 0; j < n; ++j) {
+                double a = zeta * d2[j] * (x[j] - xR[j]);
+                for (int i = 0; i < m; ++i) a -= J[i * n + j] * y[i];
+                gx[j] = a;
+            }
+        }
+        const double tau = fmax(0.99, 1.0 - mu);
+        for (int i = 0; i < m; ++i) {
+            Sp[i] = zp[i] / pp[i];
+            Sn[i] = zn[i] / nn[i];
+            Ss[i] = (hl[i] ? vl[i] / dl[i] : 0.0) + (hu[i] ? vu[i] / du[i] : 0.0);
+            D[i] = 1.0 / Sp[i] + 1.0 / Sn[i] + 1.0 / Ss[i];
+            const double mdl = hl[i] ? mu / dl[i] : 0.0, mdu = hu[i] ? mu / du[i] : 0.0;
+            const double rc = c[i] - pp[i] + nn[i] - s[i];
+            b[i] = -rc + (-rho - y[i] + mu / pp[i]) / Sp[i] - (-rho + y[i] + mu / nn[i]) / Sn[i] +
+                   (-y[i] + mdl - mdu) / Ss[i];
+        }
+        phess_of(P, x, y, 0.0, H);
+        for (int a = 0; a < n; ++a) {
+            for (int bb = 0; bb < n; ++bb) {
+                double acc = 0;
+                for (int i = 0; i < m; ++i) acc += J[i * n + a] * J[i * n + bb] / D[i];
+                Kmat[a * n + bb] = H[a * n + bb] + (a == bb ? zeta * d2[a] : 0.0) + acc;
+            }
+            double acc = -gx[a];
+            for (int i = 0; i < m; ++i) acc += J[i * n + a] * (b[i] / D[i]);
+            rhs[a] = acc;
+        }
+        memcpy(L, Kmat, sizeof(double) * n * n);
+        if (!chol(L, n)) {
+            double dw = dw_last == 0 ? 1e-4 : fmax(1e-20, dw_last / 3.0);
+            int ok = 0;
+            for (;;) {
+                memcpy(L, Kmat, sizeof(double) * n * n);
+                for (int a = 0; a < n; ++a) L[a * n + a] += dw;
+                if (chol(L, n)) {
+                    ok = 1;
+                    break;
+                }
+                dw *= dw_last == 0 ? 100.0 : 8.0;
+                if (dw > 1e40) break;
+            }
+            dw_last = dw;
+            if (!ok) {
+                ret = RS_FAILED;
+                break;
+            }
+        }
+        memcpy(dx, rhs, sizeof(double) * n);
+        cholsolve(L, n, dx);
+        double ap = 1.0, az = 1.0;
+        for (int i = 0; i < m; ++i) {
+            double jd = 0;
+            for (int j = 0; j < n; ++j) jd += J[i * n + j] * dx[j];
+            const double mdl = hl[i] ? mu / dl[i] : 0.0, mdu = hu[i] ? mu / du[i] : 0.0;
+            dy[i] = (b[i] - jd) / D[i];
+            dp[i] = (-rho - y[i] + mu / pp[i] - dy[i]) / Sp[i];
+            dn[i] = (-rho + y[i] + mu / nn[i] + dy[i]) / Sn[i];
+            ds[i] = (-y[i] + mdl - mdu - dy[i]) / Ss[i];
+            dzp[i] = mu / pp[i] - zp[i] - Sp[i] * dp[i];
+            dzn[i] = mu / nn[i] - zn[i] - Sn[i] * dn[i];
+            dvl[i] = hl[i] ? mdl - vl[i] - vl[i] / dl[i] * ds[i] : 0.0;
+            dvu[i] = hu[i] ? mdu - vu[i] + vu[i] / du[i] * ds[i] : 0.0;
+            ap = ftb(pp[i], dp[i], tau, ap);
+            ap = ftb(nn[i], dn[i], tau, ap);
+            if (hl[i]) ap = ftb(dl[i], ds[i], tau, ap);
+            if (hu[i]) ap = ftb(du[i], -ds[i], tau, ap);
+            az = ftb(zp[i], dzp[i], tau, az);
+            az = ftb(zn[i], dzn[i], tau, az);
+            if (hl[i]) az = ftb(vl[i], dvl[i], tau, az);
+            if (hu[i]) az = ftb(vu[i], dvu[i], tau, az);
+        }
+        double theta = 0, q0 = 0, gphi = 0, lg = 0;
+        int bad = 0;
+        for (int j = 0; j < n; ++j) {
+            q0 += d2[j] * (x[j] - xR[j]) * (x[j] - xR[j]);
+            gphi += zeta * d2[j] * (x[j] - xR[j]) * dx[j];
+        }
+        double spn = 0, gpn = 0, gs = 0;
+        for (int i = 0; i < m; ++i) {
+            theta += fabs(c[i] - pp[i] + nn[i] - s[i]);
+            spn += pp[i] + nn[i];
+            gpn += (rho - mu / pp[i]) * dp[i] + (rho - mu / nn[i]) * dn[i];
+            gs += (hl[i] ? mu * ds[i] / dl[i] : 0.0) - (hu[i] ? mu * ds[i] / du[i] : 0.0);
+            lg += log(pp[i]) + log(nn[i]);
+            if (hl[i]) lg += log(dl[i]);
+            if (hu[i]) lg += log(du[i]);
+        }
+        (void)bad;
+        gphi += gpn - gs;
+        const double phi = rho * spn + 0.5 * zeta * q0 - mu * lg;
+        double amin;
+        if (gphi < 0) {
+            amin = fmin(gth, gph * theta / -gphi);
+            if (theta <= theta_min) amin = fmin(amin, pow(theta, sth) / pow(-gphi, sph));
+        } else
+            amin = gth;
+        amin *= gal;
+        if (!(amin > 0.0)) amin = 8.673617379884035e-19;
+        double al = ap;
+        int accepted = 0, ftype = 0;
+        while (al >= amin) {
+            for (int j = 0; j < n; ++j) xt[j] = x[j] + al * dx[j];
+            for (int i = 0; i < m; ++i) {
+                pt[i] = pp[i] + al * dp[i];
+                nt[i] = nn[i] + al * dn[i];
+                st[i] = s[i] + al * ds[i];
+            }
+            pcons(P, xt, ct);
+            double tht = 0, qt = 0, spt = 0, lgt = 0;
+            int badt = 0;
+            for (int j = 0; j < n; ++j) qt += d2[j] * (xt[j] - xR[j]) * (xt[j] - xR[j]);
+            for (int i = 0; i < m; ++i) {
+                tht += fabs(ct[i] - pt[i] + nt[i] - st[i]);
+                spt += pt[i] + nt[i];
+                if (!(pt[i] > 0) || !(nt[i] > 0)) badt = 1;
+                if (hl[i] && !(st[i] - cl[i] > 0)) badt = 1;
+                if (hu[i] && !(cu[i] - st[i] > 0)) badt = 1;
+                if (!badt) {
+                    lgt += log(pt[i]) + log(nt[i]);
+                    if (hl[i]) lgt += log(st[i] - cl[i]);
+                    if (hu[i]) lgt += log(cu[i] - st[i]);
+                }
+            }
+            const double pht = badt ? INFINITY : rho * spt + 0.5 * zeta * qt - mu * lgt;
+            int ok = isfinite(pht) && tht < theta_max;
+            for (int q = 0; ok && q < nf; ++q)
+                if (!(tht < ft[2 * q] || pht < ft[2 * q + 1])) ok = 0;
+            if (ok) {
+                int switching = gphi < 0 && al * pow(-gphi, sph) > pow(theta, sth);
+                if (switching && theta <= theta_min) {
+                    if (pht <= phi + eta * al * gphi) {
+                        accepted = 1;
+                        ftype = 1;
+                    }
+                } else if (tht <= (1 - gth) * theta || pht <= phi - gph * theta) {
+                    accepted = 1;
+                    ftype = 0;
+                }
+            }
+            if (accepted) break;
+            al *= 0.5;
+        }
+        if (!accepted) {
+            ret = RS_FAILED;
+            break;
+        }
+        if (!ftype && nf < maxf) {
+            ft[2 * nf] = (1 - gth) * theta;
+            ft[2 * nf + 1] = phi - gph * theta;
+            nf++;
+        }
+        memcpy(x, xt, sizeof(double) * n);
+        for (int i = 0; i < m; ++i) {
+            pp[i] = pt[i];
+            nn[i] = nt[i];
+            s[i] = st[i];
+            y[i] += al * dy[i];
+            zp[i] += az * dzp[i];
+            zn[i] += az * dzn[i];
+            vl[i] += az * dvl[i];
+            vu[i] += az * dvu[i];
+            const double ks = 1e10;
+            zp[i] = fmin(fmax(zp[i], mu / (ks * pp[i])), ks * mu / pp[i]);
+            zn[i] = fmin(fmax(zn[i], mu / (ks * nn[i])), ks * mu / nn[i]);
+            if (hl[i]) {
+                double d = s[i] - cl[i];
+                vl[i] = fmin(fmax(vl[i], mu / (ks * d)), ks * mu / d);
+            } else
+                vl[i] = 0;
+            if (hu[i]) {
+                double d = cu[i] - s[i];
+                vu[i] = fmin(fmax(vu[i], mu / (ks * d)), ks * mu / d);
+            } else
+                vu[i] = 0;
+        }
+        ++*it;
+    }
+    free(ft);
+    return ret;
 }
 
 /* Primal-dual interior point with IPOPT's filter line search; mirrors np_oracle.solve. */
@@ -1090,7 +1424,7 @@ static void osolve(oprob* P, const double* u0, double* uout, osolve_info* info)
     double gf[OMAXV], J[OMAXM * OMAXV], H[OMAXV * OMAXV], Kmat[OMAXV * OMAXV], rhs[OMAXV], y[OMAXM];
     double dl[OMAXM], du[OMAXM], rc[OMAXM], Sig[OMAXM], dU[OMAXV], dS[OMAXM], dZl[OMAXM], dZu[OMAXM];
     double ut[OMAXV], st[OMAXM], ct[OMAXM];
-    for (it = 0; it <= cfg->max_iter; ++it) {
+    for (it = 0; it <= cfg->max_iter;) {
         /* cfg.goal_singular = ABORT: the reference's NaN gradient at this iterate — IPOPT's Eval_Error, status
            Invalid_Number_Detected with the iterate returned (include/alipmpc.h) */
         if (cfg->goal_singular == ALIPMPC_GOAL_SINGULAR_ABORT && at_goal(P, u)) {
@@ -1132,7 +1466,7 @@ static void osolve(oprob* P, const double* u0, double* uout, osolve_info* info)
             status = 0;
             break;
         }
-        if (it == cfg->max_iter) break;
+        if (it >= cfg->max_iter) break;
         /* IPOPT's floor min(tol, compl_inf_tol) / (barrier_tol_factor + 1 = 11) (MonotoneMuUpdate): tol / 11 for
            tol <= compl_inf_tol = 1e-4 (the fp32 programs' larger tolerances keep tol / 11) */
         double mu_min = cfg->tol / 11.0, mu_old = mu;
@@ -1257,6 +1591,35 @@ static void osolve(oprob* P, const double* u0, double* uout, osolve_info* info)
             memcpy(u, ut, sizeof(double) * n);
             memcpy(s, st, sizeof(double) * m);
             memcpy(c, ct, sizeof(double) * m);
+        } else if (cfg->restoration == ALIPMPC_RESTORATION_IPOPT && !P->dd) {
+            /* IPOPT: the current point enters the filter, then the restoration phase takes over (oresto) */
+            n_rest++;
+            if (nf < maxf) {
+                ft[2 * nf] = (1 - gth) * theta;
+                ft[2 * nf + 1] = phi - gph * theta;
+                nf++;
+            }
+            it++;
+            const int rs = oresto(P, u, s, zl, zu, mu, cl, cu, hl, hu, ft, nf, theta, &it, cfg->max_iter, cfg->tol);
+            pcons(P, u, c);
+            if (rs == RS_INFEASIBLE || rs == RS_FAILED) {
+                status = 2;
+                break;
+            }
+            if (rs == RS_MAXITER) break;
+            for (int i = 0; i < m; ++i) {
+                if (hl[i]) {
+                    double d = s[i] - cl[i];
+                    zl[i] = fmin(fmax(zl[i], mu / (1e10 * d)), 1e10 * mu / d);
+                } else
+                    zl[i] = 0;
+                if (hu[i]) {
+                    double d = cu[i] - s[i];
+                    zu[i] = fmin(fmax(zu[i], mu / (1e10 * d)), 1e10 * mu / d);
+                } else
+                    zu[i] = 0;
+            }
+            continue;
         } else {
             n_rest++;
             a = fmax(a, amin);
@@ -1290,6 +1653,7 @@ static void osolve(oprob* P, const double* u0, double* uout, osolve_info* info)
                 zu[i] = 0;
         }
 #undef ERR
+        ++it;
     }
     free(ft);
     if (status != 0 && status != 2 && status != -3 && status != ALIPMPC_INVALID_NUMBER_DETECTED) {
