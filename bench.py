@@ -195,6 +195,11 @@ def main():
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     status = out["status"].cpu().numpy()
     iters = out["iters"].cpu().numpy()
+    # lane program + IPOPT's restoration phase: instances whose line search failed are solved by the fp64 wave program
+    try:
+        handoffs = solver.lane_handoffs(stream) if program == "lane" else 0
+    except (AttributeError, RuntimeError):
+        handoffs = None
     B_total = B_total_of(preset, args, B, world)
     total_solves = B_total * K
     value = total_solves / elapsed
@@ -263,18 +268,23 @@ def main():
                             f"= the reference's IPOPT cap)",
                 "batch_per_gpu": B, "global_batch": B_total, "horizon": N, "obstacles": n_cir + n_elp,
                 "variant": args.variant, "parallelism": f"shard{world}" if world > 1 else "single",
+                "restoration": "ipopt" if cfg.restoration == alipmpc.RESTORATION_IPOPT else "substitute",
                 "mean_iters": float(iters.mean()), "max_iters": int(iters.max()),
                 "status_counts": {str(k): int(v) for k, v in zip(*np.unique(status, return_counts=True))},
                 "resident_slots": slots,
                 "program": program,
-                "launch": ("persistent work queue, one instance per lane" if program == "lane" else
+                "launch": ("persistent work queue, one instance per lane" +
+                           (f"; {handoffs} instances with a failed line search handed to the fp64 wave program's "
+                            f"restoration-capable work queue (IPOPT's restoration phase)" if handoffs else "")
+                           if program == "lane" else
                            ("split launch: phase 1 one wavefront per instance up to the iteration cut, phase 2 "
                             "resumes the unfinished instances" + (" (trial-cut ones on 4-wave teams)" if team > 1 else
                                                                   " one wavefront each"))
                            if launches == 2 else
                            "one wavefront per instance (B <= resident slots, no queue)" if slots and B <= slots else
                            "persistent work queue, one instance per wavefront"),
-                "launches_per_solve": launches,
+                "launches_per_solve": launches + (1 if handoffs else 0),
+                "lane_handoffs": handoffs if program == "lane" else None,
                 "build_id": bid,
             },
             "roofline": {
@@ -555,6 +565,7 @@ def cpu_baseline(cfg, batch, seconds, threads=1, workload="cfg2"):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as C
     co = C.default_cfg(cfg.variant, cfg.N, nc_max=cfg.nc_max, ne_max=cfg.ne_max)
+    co.restoration = cfg.restoration
     B = batch["x0"].shape[0]
     ne_max = cfg.ne_max
     elp = batch["elp"] if ne_max else None

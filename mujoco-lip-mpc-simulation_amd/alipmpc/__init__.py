@@ -8,10 +8,10 @@ from ._lib import (Cfg, Solver, default_cfg, load, lib_path, build_id, num_vars,
                    VARIANT_MODI, VARIANT_SIG_STEP, VARIANT_DD, PREC_FP64, PREC_FP32, PROGRAM_WAVE, PROGRAM_LANE,
                    ROLLOUT_DONE, FP32_TOL,
                    FP32_ACCEPTABLE_TOL, FP32_TOL_LONG, FP32_ACCEPTABLE_TOL_LONG, GOAL_SINGULAR_ZERO,
-                   GOAL_SINGULAR_ABORT, INVALID_NUMBER_DETECTED)
+                   GOAL_SINGULAR_ABORT, INVALID_NUMBER_DETECTED, RESTORATION_IPOPT, RESTORATION_SUBSTITUTE)
 
 __all__ = ["Cfg", "Solver", "default_cfg", "load", "lib_path", "build_id", "num_vars", "rows_per_step", "trace_len", "EXPORTS",
            "STATUS_NAMES", "VARIANT_MODI", "VARIANT_SIG_STEP", "VARIANT_DD", "PREC_FP64", "PREC_FP32",
            "PROGRAM_WAVE", "PROGRAM_LANE", "ROLLOUT_DONE", "FP32_TOL", "FP32_ACCEPTABLE_TOL",
            "FP32_TOL_LONG", "FP32_ACCEPTABLE_TOL_LONG", "GOAL_SINGULAR_ZERO", "GOAL_SINGULAR_ABORT",
-           "INVALID_NUMBER_DETECTED"]
+           "INVALID_NUMBER_DETECTED", "RESTORATION_IPOPT", "RESTORATION_SUBSTITUTE"]

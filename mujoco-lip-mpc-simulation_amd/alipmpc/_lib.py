@@ -16,6 +16,7 @@ VARIANT_MODI, VARIANT_SIG_STEP, VARIANT_DD = 0, 1, 2
 PREC_FP64, PREC_FP32 = 0, 1
 PROGRAM_WAVE, PROGRAM_LANE = 0, 1   # cfg.program: one instance per wavefront / per lane (include/alipmpc.h)
 GOAL_SINGULAR_ZERO, GOAL_SINGULAR_ABORT = 0, 1   # cfg.goal_singular (include/alipmpc.h)
+RESTORATION_IPOPT, RESTORATION_SUBSTITUTE = 0, 1   # cfg.restoration (include/alipmpc.h)
 INVALID_NUMBER_DETECTED = -13
 
 STATUS_NAMES = {0: "Solve_Succeeded", 1: "Solved_To_Acceptable_Level", 2: "Infeasible_Problem_Detected",
@@ -44,7 +45,7 @@ class Cfg(ctypes.Structure):
 EXPORTS = ("alipmpc_default_cfg", "alipmpc_rows_per_step", "alipmpc_num_vars", "alipmpc_create",
            "alipmpc_solve_batch", "alipmpc_eval_batch", "alipmpc_rollout_batch", "alipmpc_closed_loop_batch",
            "alipmpc_trace_len",
-           "alipmpc_trace_batch", "alipmpc_nominal_gait_batch", "alipmpc_solve_slots", "alipmpc_solve_launches", "alipmpc_solve_program", "alipmpc_last_kernel_ms",
+           "alipmpc_trace_batch", "alipmpc_nominal_gait_batch", "alipmpc_solve_slots", "alipmpc_solve_launches", "alipmpc_lane_handoffs", "alipmpc_solve_program", "alipmpc_last_kernel_ms",
            "alipmpc_build_id",
            "alipmpc_last_error", "alipmpc_destroy")
 
@@ -99,6 +100,9 @@ def load(build_if_missing=True):
     if hasattr(L, "alipmpc_nominal_gait_batch"):   # (absent from older dev builds used for A/B timing)
         L.alipmpc_nominal_gait_batch.argtypes = [P, ctypes.c_int64, ctypes.c_double, P, P, P, P, P, P]
         L.alipmpc_nominal_gait_batch.restype = ctypes.c_int
+    if hasattr(L, "alipmpc_lane_handoffs"):
+        L.alipmpc_lane_handoffs.argtypes = [P, P, ctypes.POINTER(ctypes.c_int64)]
+        L.alipmpc_lane_handoffs.restype = ctypes.c_int
     if hasattr(L, "alipmpc_solve_launches"):
         L.alipmpc_solve_launches.argtypes = [P, ctypes.c_int64, ctypes.POINTER(ctypes.c_int32),
                                              ctypes.POINTER(ctypes.c_int32)]
@@ -232,6 +236,14 @@ class Solver:
         self._check(self._L.alipmpc_solve_launches(self._h, int(B), ctypes.byref(n), ctypes.byref(t)),
                     "alipmpc_solve_launches")
         return int(n.value), int(t.value)
+
+    def lane_handoffs(self, stream=None):
+        """Instances of the last lane-program solve on `stream` (None: the handle's own stream, the host-pointer calls)
+        that were handed to the fp64 wave program for IPOPT's restoration phase (include/alipmpc.h)."""
+        v = ctypes.c_int64(0)
+        st = None if stream is None else _stream_arg(stream)
+        self._check(self._L.alipmpc_lane_handoffs(self._h, st, ctypes.byref(v)), "alipmpc_lane_handoffs")
+        return int(v.value)
 
     # ---------------------------------------------------------------- host (numpy) calls
     def _inputs(self, x0, goal, leg, cir, nc, elp, ne):

@@ -19,6 +19,7 @@ REPO = os.path.dirname(ROOT)
 SRC = os.path.join(ROOT, "csrc", "alipmpc.hip")
 INC = os.path.join(ROOT, "csrc", "lane_solve.inc")
 MATH = os.path.join(ROOT, "csrc", "fastmath.inc")
+RESTO = os.path.join(ROOT, "csrc", "resto_wave.inc")
 HDR = os.path.join(REPO, "include", "alipmpc.h")
 LIB = os.path.join(PKG, "libalipmpc.so")
 PARTS = range(0, 9)
@@ -37,7 +38,7 @@ def build_id(extra=(), src=None):
     and the extra flags.  Compiled into the library (alipmpc_build_id) so a counter record made with one build is
     never attached to a bench line of another (tools/roofline.py, bench.py)."""
     h = hashlib.sha256()
-    for p in (src or SRC, INC, MATH, HDR):
+    for p in (src or SRC, INC, MATH, RESTO, HDR):
         with open(p, "rb") as fh:
             h.update(fh.read())
     h.update(" ".join([*ARCH, *FLAGS, *extra]).encode())
@@ -48,7 +49,7 @@ def needs_build():
     if not os.path.exists(LIB):
         return True
     t = os.path.getmtime(LIB)
-    return any(os.path.getmtime(p) > t for p in (SRC, INC, MATH, HDR, __file__))
+    return any(os.path.getmtime(p) > t for p in (SRC, INC, MATH, RESTO, HDR, __file__))
 
 
 def _run(cmd, verbose):

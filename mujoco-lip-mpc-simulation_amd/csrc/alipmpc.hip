@@ -66,6 +66,10 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 struct KP {
     int nc_max, ne_max, rps, m_max, mr4, mo4, modi, max_iter, select_obs, detour;
     int goal_abort;   // cfg.goal_singular == ABORT: an iterate with a planned state on the goal ends with status -13
+    int resto_ipopt;  // cfg.restoration == IPOPT (LIP variants): a failed line search enters IPOPT's restoration phase
+    uint32_t* redo;          // lane program, cfg.restoration = IPOPT: [0] = count, then the instances whose line search
+                             // failed (their solve is handed to the fp64 wave program, which has the restoration phase)
+    const uint32_t* bcount;  // nullable: the work-queue form solves instances order[k] for k < min(B, *bcount)
     double tol, acc_tol, q, p, r, gm1, s, detect_r2, leg2, bvx_lo, bvx_hi, bvy_lo, bvy_hi, dth, mu_init, dt, dd_t;
     const double* G;   // NG x NCP
     const double* E;   // NG x 5
@@ -156,6 +160,7 @@ constexpr int TEAM_WAVES = ALIP_TEAM_WAVES;
 #define ALIP_GJ_MAX_N 15  // (cfg3, n = 15: 16.14 -> 15.51 ms per launch against the Cholesky)
 #endif
 constexpr int ST_CKPT = 3;   // internal status of an instance whose loop state went to a split-launch record
+constexpr int ST_RESTO = 4;  // internal: a failed line search hands the point to IPOPT's restoration phase
 // record slots are doubles; an fp32 kernel's values are stored as their bit patterns (no conversion)
 __device__ __forceinline__ double ck_put(double v) { return v; }
 __device__ __forceinline__ double ck_put(float v) { return __longlong_as_double((long long)__float_as_uint(v)); }
@@ -1194,6 +1199,7 @@ template <int N, class R>
 __device__ void hess_blocks_lanes(const WSS<N, R>& w, int lane, int rps, int nobs, int modi)
 {
     static_assert(16 * (N + 1) <= WAVE, "one 16-lane row per block");
+    static_assert(ALIPMPC_MAX_OBS <= 32, "lane j takes obstacle slots j and j + 16 only (ADVICE r5)");
     const int kb = lane >> 4, j = lane & 15;
     const R gm1 = w.cst[K_GM1];
     R t00 = R(0), t01 = R(0), t11 = R(0);
@@ -1273,11 +1279,17 @@ __device__ __forceinline__ R obj_sum(const R (&v)[RPL], int mr4)
 template <int N, int RPL>
 constexpr bool TEAM_HANDOVER = 3 * WAVE * RPL + 3 <= Dim<N>::NCP * Dim<N>::KLD;
 
+#include "resto_wave.inc"
+
 // TM: the team-capable build (split launches with team records, solve_kernel<..., TM = true>): phase 1 also cuts an
 // instance by its line-search trial count, phase 2 runs team records on 4 waves; tm < 0 = member -1 - tm of a team.
 // Without TM all of it compiles out: the interior-point loop of the plain build sits at its register budget, and the
 // team logic in the same body had cost 36 -> 172 B/lane of spills (the register allocator, not the arithmetic).
-template <int N, int KSM, class R, bool Q, bool TM = false>
+// RS: the restoration-capable build (cfg.restoration = IPOPT): a failed line search runs IPOPT's restoration phase
+// (resto_wave.inc, inlined) at the top of the next iteration.  The lean build (RS = false: phase 1 of a split launch)
+// instead cuts the instance to a split record flagged "restoration pending", and phase 2's RS build runs the phase
+// first — so the restoration's registers never touch the lean loop that most instances finish in.
+template <int N, int KSM, class R, bool Q, bool TM = false, bool RS = false>
 __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* wsb, int wv, long long b, long long rec = -1,
                                           int tm = 0)
 {
@@ -1499,6 +1511,10 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* wsb, int wv, lo
     R e0 = INFINITY;
     R theta_c = R(0.0);
     bool theta_ok = false;
+    // restoration pending (cfg.restoration = IPOPT): the line search of the last iteration failed at the current point,
+    // whose violation theta_R entered the filter
+    bool rpend = false;
+    R theta_R = R(0.0);
     const R gth = R(1e-5), gph = R(1e-8), sth = R(1.1), sph = R(2.3), eta = R(1e-8), gal = R(0.05);
 
     int it0 = 0;
@@ -1538,6 +1554,10 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* wsb, int wv, lo
         fail_it = rfl((int)sc[8]);
         it_end = rfl((int)sc[9]);
         theta_ok = rfl((int)sc[10]) != 0;
+        if constexpr (RS) {   // (a lean-build record: the restoration pending at its point)
+            rpend = rfl((int)sc[11]) != 0;
+            theta_R = uni(ck_get<R>(sc[12]));
+        }
         if (lane < NG) w.V[lane] = vme;
         wave_sync();
 #ifndef ALIP_NO_SETPRIO
@@ -1556,47 +1576,114 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* wsb, int wv, lo
     const int ckpt_it = TM && tm < 0 ? 0 : rfl(P.ckpt_it);
     const int ckpt_tr = TM && tm >= 0 ? rfl(P.team > 0 ? P.ckpt_tr : 0) : 0;
     STAMP_DECL
-    for (it = it0; it <= max_iter; ++it) {
+    // the loop state as a split record (record k of the launch): phase 2 resumes it exactly (rp: a restoration is
+    // pending at this point, theta_R its violation)
+    auto put_record = [&](bool to_team, bool rp) {
+        int k = 0;
+        if (lane == 0)
+            k = to_team ? (int)(P.B - 1 - (long long)atomicAdd(P.cont + CONT_TEAM, 1u))
+                        : (int)atomicAdd(P.cont + CONT_SINGLE, 1u);
+        k = rfl(k);
+        double* rc = P.ckpt + (long long)k * ckpt_doubles(RPL);
+#pragma unroll
+        for (int q = 0; q < RPL; ++q) {
+            double* rq = rc + WAVE * CKPT_ROW * q + lane;
+            rq[0] = ck_put(sr[q]);
+            rq[WAVE] = ck_put(zl[q]);
+            rq[2 * WAVE] = ck_put(zu[q]);
+            rq[3 * WAVE] = ck_put(idl[q]);
+            rq[4 * WAVE] = ck_put(idu[q]);
+            rq[5 * WAVE] = ck_put(cr[q]);
+            rq[6 * WAVE] = ck_put(ra0[q]);
+            rq[7 * WAVE] = ck_put(ra1[q]);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) rq[(8 + i) * WAVE] = ck_put(rv[q][i]);
+        }
+        double* rf = rc + WAVE * CKPT_ROW * RPL + lane;
+        rf[0] = ck_put(fth0);
+        rf[WAVE] = ck_put(fph0);
+        rf[2 * WAVE] = ck_put(fth1);
+        rf[3 * WAVE] = ck_put(fph1);
+        rf[4 * WAVE] = ck_put(vme);
+        const double sv[13] = {ck_put(mu), ck_put(f_cur), ck_put(lsum_cur), ck_put(theta_c), ck_put(dw_last),
+                               (double)nf, (double)it, (double)n_rest, (double)fail_it, (double)it_end,
+                               theta_ok ? 1.0 : 0.0, rp ? 1.0 : 0.0, ck_put(theta_R)};
+        double v = 0.0;
+#pragma unroll
+        for (int i = 0; i < 13; ++i) v = lane == i ? sv[i] : v;
+        if (lane < 13) rc[WAVE * (CKPT_ROW * RPL + 5) + lane] = v;
+        if (lane == 0) P.cont[cont_hdr(P.B) + k] = (uint32_t)b;
+    };
+    R phi_R = R(0.0);
+    it = it0;
+    // regular iterations; with cfg.restoration = IPOPT a failed line search leaves this loop (ST_RESTO) and IPOPT's
+    // restoration phase runs between two passes of it (RS build) or in phase 2 (the lean build cuts the instance)
+    for (;;) {
+    if constexpr (RS) {
+        if (rpend) {
+            // IPOPT's restoration phase from the failed point (the current iterate, slacks and multipliers; the
+            // augmented filter; theta_R), resto_wave.inc; its iterate comes back through the workspace
+            rpend = false;
+            RELANE();
+#pragma unroll
+            for (int q = 0; q < RPL; ++q) {
+                const int r = lane + WAVE * q;
+                if (r < mo4) {
+                    w.ry[r] = sr[q];
+                    w.rsig[r] = zl[q];
+                    w.rw[r] = zu[q];
+                }
+            }
+            if (lane < NG) w.V[lane] = vme;
+            wave_sync();
+            const int rr = rfl(resto_wave<N, KSM, R>(wv, fth0, fph0, fth1, fph1, nf, mu, theta_R, it));
+            const int rcode = rr & 15;
+            it = rr >> 4;
+            RELANE();
+            vme = lane < NG ? w.V[lane] : R(0.0);
+            R lr = R(0.0);
+#pragma unroll
+            for (int q = 0; q < RPL; ++q) {
+                const int r = lane + WAVE * q;
+                if (r < mo4) {
+                    sr[q] = w.ry[r];
+                    zl[q] = w.rsig[r];
+                    zu[q] = w.rw[r];
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i) rv[q][i] = w.V[gen_i(rg[q], i)];
+                R o[6];
+#pragma unroll
+                for (int i = 0; i < 6; ++i) o[i] = w.obs6[6 * roi[q] + i];
+                row_trans(rtype[q], rv[q], w.cst[K_GXG], w.cst[K_GYG], ra0[q], ra1[q]);
+                cr[q] = row_value(rtype[q], rk[q], rv[q], ra0[q], ra1[q], o, CK);
+                const R d1 = sr[q] - cl[q], d2 = cu[q] - sr[q];
+                lr += llog(HL(q) ? (HU(q) ? d1 * d2 : d1) : (HU(q) ? d2 : R(1.0)));
+                // (kappa_sigma safeguard with the regular barrier parameter, as after every iteration)
+                idl[q] = HL(q) ? rcp_nr(d1) : R(0.0);
+                idu[q] = HU(q) ? rcp_nr(d2) : R(0.0);
+                zl[q] = HL(q) ? fmin(fmax(zl[q], mu * R(1e-10) * idl[q]), R(1e10) * mu * idl[q]) : R(0.0);
+                zu[q] = HU(q) ? fmin(fmax(zu[q], mu * R(1e-10) * idu[q]), R(1e10) * mu * idu[q]) : R(0.0);
+            }
+            lsum_cur = wsum(lr);
+            f_cur = obj_sum<N, RPL>(cr, mr4);
+            theta_ok = false;
+            wave_sync();
+            if (rcode == RSW_INFEASIBLE || rcode == RSW_FAILED) {   // Infeasible_Problem_Detected
+                status = 2;
+                break;
+            }
+            if (rcode == RSW_MAXITER) break;   // the cap inside the restoration: the final status test below
+        }
+    }
+    for (; it <= max_iter; ++it) {
         // split launch, phase 1: an instance still running at iteration ckpt_it writes its loop state to the next
         // record and stops; phase 2 resumes it on a wave of its own (the long instances no longer share SIMDs).
         // Team-capable build: an instance whose line searches have run ckpt_tr trials (a long search every
         // iteration) stops early and writes a TEAM record, which phase 2 resumes on a workgroup's 4 waves
+        // (the cuts run in the lean build, whose count never jumps: a restoration there is cut itself)
         if ((ckpt_it > 0 && it == ckpt_it) || (TM && ckpt_tr > 0 && w.cst[K_NTR] >= R(ckpt_tr))) {
-            const bool to_team = TM && !(ckpt_it > 0 && it == ckpt_it);
-            int k = 0;
-            if (lane == 0)
-                k = to_team ? (int)(P.B - 1 - (long long)atomicAdd(P.cont + CONT_TEAM, 1u))
-                            : (int)atomicAdd(P.cont + CONT_SINGLE, 1u);
-            k = rfl(k);
-            double* rc = P.ckpt + (long long)k * ckpt_doubles(RPL);
-#pragma unroll
-            for (int q = 0; q < RPL; ++q) {
-                double* rq = rc + WAVE * CKPT_ROW * q + lane;
-                rq[0] = ck_put(sr[q]);
-                rq[WAVE] = ck_put(zl[q]);
-                rq[2 * WAVE] = ck_put(zu[q]);
-                rq[3 * WAVE] = ck_put(idl[q]);
-                rq[4 * WAVE] = ck_put(idu[q]);
-                rq[5 * WAVE] = ck_put(cr[q]);
-                rq[6 * WAVE] = ck_put(ra0[q]);
-                rq[7 * WAVE] = ck_put(ra1[q]);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) rq[(8 + i) * WAVE] = ck_put(rv[q][i]);
-            }
-            double* rf = rc + WAVE * CKPT_ROW * RPL + lane;
-            rf[0] = ck_put(fth0);
-            rf[WAVE] = ck_put(fph0);
-            rf[2 * WAVE] = ck_put(fth1);
-            rf[3 * WAVE] = ck_put(fph1);
-            rf[4 * WAVE] = ck_put(vme);
-            const double sv[11] = {ck_put(mu), ck_put(f_cur), ck_put(lsum_cur), ck_put(theta_c), ck_put(dw_last),
-                                   (double)nf, (double)it, (double)n_rest, (double)fail_it, (double)it_end,
-                                   theta_ok ? 1.0 : 0.0};
-            double v = 0.0;
-#pragma unroll
-            for (int i = 0; i < 11; ++i) v = lane == i ? sv[i] : v;
-            if (lane < 11) rc[WAVE * (CKPT_ROW * RPL + 5) + lane] = v;
-            if (lane == 0) P.cont[cont_hdr(P.B) + k] = (uint32_t)b;
+            put_record(TM && !(ckpt_it > 0 && it == ckpt_it), false);
             status = ST_CKPT;
             break;
         }
@@ -2223,6 +2310,12 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* wsb, int wv, lo
             lsum_cur = lgt;
             theta_c = tht_acc;
             theta_ok = true;
+        } else if (rfl(P.resto_ipopt)) {
+            // cfg.restoration = IPOPT: the failed point (this iteration counts) goes to the restoration phase after
+            // this loop
+            status = ST_RESTO;
+            it++;
+            break;
         } else {
             theta_ok = false;
             // restoration substitute: shortest tried step, slacks reset onto c(u), filter reset
@@ -2289,6 +2382,41 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* wsb, int wv, lo
         }
         wave_sync();
         STAMP(9);
+    }
+    if (status != ST_RESTO) break;
+    // the failed point (this iteration counted) enters the filter — IPOPT's augmented filter, with the point's
+    // violation (the same sum as the iteration's theta) and barrier function — then the restoration phase from it
+    ++n_rest;
+    {
+        RELANE();
+        R th = R(0.0);
+#pragma unroll
+        for (int q = 0; q < RPL; ++q)
+            if (rtype[q] < R_NONE) th += fabs(cr[q] - sr[q]);
+        theta_R = theta_ok ? theta_c : wsum(th);
+        phi_R = uni(f_cur - mu * lsum_cur);
+    }
+    if (nf < FILTER_CAP) {
+        const R fvt = (1 - gth) * theta_R, fvp = phi_R - gph * theta_R;
+        if ((nf & (WAVE - 1)) == lane) {
+            if (nf < WAVE) {
+                fth0 = fvt;
+                fph0 = fvp;
+            } else {
+                fth1 = fvt;
+                fph1 = fvp;
+            }
+        }
+        nf++;
+    }
+    theta_ok = false;
+    status = -1;
+    if constexpr (!RS) {   // the lean build (phase 1 of a split launch): phase 2's RS build runs the phase
+        put_record(false, true);
+        status = ST_CKPT;
+        break;
+    }
+    rpend = true;
     }
     STAMP(8);
     STAMP_FLUSH;
@@ -2376,8 +2504,17 @@ __device__ __forceinline__ void queue_exit(uint32_t* q)
 #ifndef ALIP_WAVES_F32
 #define ALIP_WAVES_F32 7
 #endif
-template <int KSM, class R>
-constexpr int solve_waves() { return 4 * KSM > WAVE ? ALIP_WAVES_RPL2 : (sizeof(R) == 4 ? ALIP_WAVES_F32 : ALIP_WAVES_RPL1); }
+#ifndef ALIP_WAVES_RS
+#define ALIP_WAVES_RS 2
+#endif
+template <int KSM, class R, bool RSW = false>
+constexpr int solve_waves()
+{
+    // RSW: the restoration-capable build of the one-wave-per-instance form (split phase 2, one-phase launches): its
+    // instances run on lone waves, so it takes the registers of 2 waves per SIMD (fp32: 4) instead of spilling
+    return 4 * KSM > WAVE ? ALIP_WAVES_RPL2
+                          : (RSW ? (sizeof(R) == 4 ? 4 : ALIP_WAVES_RS) : (sizeof(R) == 4 ? ALIP_WAVES_F32 : ALIP_WAVES_RPL1));
+}
 
 // Launch forms of one solve program.  A batch larger than the resident slots runs the persistent work queue:
 // a grid of the resident workgroups whose waves take instances with one atomicAdd each, so a wave that
@@ -2388,8 +2525,8 @@ constexpr int solve_waves() { return 4 * KSM > WAVE ? ALIP_WAVES_RPL2 : (sizeof(
 // solve_one and produce the same bits for an instance (test_work_queue_batch_independence solves a batch
 // above the slots whole and in half-slot chunks and compares status, iters, u, foot, x_pred exactly), so an
 // instance's result does not depend on its batch or on the device's slot count.
-template <int N, int KSM, class R, bool ONE, bool TM = false>
-__global__ __launch_bounds__(WAVE * (TM ? TEAM_WAVES : WAVES_PER_BLOCK), (solve_waves<KSM, R>())) void solve_kernel(KP Pv)
+template <int N, int KSM, class R, bool ONE, bool TM = false, bool RS = false>
+__global__ __launch_bounds__(WAVE * (TM ? TEAM_WAVES : WAVES_PER_BLOCK), (solve_waves<KSM, R, RS && ONE>())) void solve_kernel(KP Pv)
 {
     constexpr int WPB = TM ? TEAM_WAVES : WAVES_PER_BLOCK;   // waves per workgroup (team-capable: the team size)
     using D = Dim<N>;
@@ -2435,16 +2572,18 @@ __global__ __launch_bounds__(WAVE * (TM ? TEAM_WAVES : WAVES_PER_BLOCK), (solve_
         rec = __builtin_amdgcn_readfirstlane((int)rec);
         // (one call site: the team solves run the very machine code of the single ones — two inlined copies had
         // rounded differently)
-        if (b >= 0) solve_one<N, KSM, R, false, TM>(P, G, wsb, wv, b, rec, team ? -1 - wv : 0);
+        if (b >= 0) solve_one<N, KSM, R, false, TM, RS>(P, G, wsb, wv, b, rec, team ? -1 - wv : 0);
     } else {
         uint32_t* const q = Pv.queue;
-        for (long long k = next_instance(q); k < Pv.B; k = next_instance(q)) {
+        // (a hand-off launch: the count of the list it solves was written on the device by the launch before it)
+        const long long Bq = Pv.bcount ? std::min(Pv.B, (long long)__builtin_amdgcn_readfirstlane((int)*Pv.bcount)) : Pv.B;
+        for (long long k = next_instance(q); k < Bq; k = next_instance(q)) {
             const long long b = Pv.order ? (long long)__builtin_amdgcn_readfirstlane(Pv.order[k]) : k;
             // (no split records in this form; the record index is opaque so that both forms compile the same
             // solve_one — fp32 contraction / packing decisions otherwise differ between them)
             long long rec = -1;
             asm volatile("" : "+s"(rec));
-            if (!Pv.active || Pv.active[b]) solve_one<N, KSM, R, true>(P, G, wsb, wv, b, rec);   // rollout: skip finished
+            if (!Pv.active || Pv.active[b]) solve_one<N, KSM, R, true, false, RS>(P, G, wsb, wv, b, rec);   // rollout: skip finished
         }
         queue_exit(q);
     }
@@ -4591,7 +4730,13 @@ static void set_smem(const void* f, size_t smem)
     auto& d = done[dev & 63];
     auto it = d.find(f);
     if (it != d.end() && it->second >= smem) return;
-    (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    // (r5a: at N = 6 this call failed for a kernel variant that was not launched — its workgroup's LDS above the CU's
+    // 160 KB — and the error it left was picked up by the launch's hipGetLastError, so every N = 6 solve reported
+    // "invalid argument".  A failure is consumed here; launching a kernel whose LDS does not fit fails on its own.)
+    if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem) != hipSuccess) {
+        (void)hipGetLastError();
+        return;
+    }
     d[f] = smem;
 }
 
@@ -4643,7 +4788,7 @@ void launch_solve(const KP& P0, size_t smem, hipStream_t st, unsigned* res_out)
             *res_out = res;
             return;
         }
-        if (res > 0 && need > res && !P0.resume)   // the persistent work queue over the resident workgroups
+        if (res > 0 && (need > res || P0.bcount) && !P0.resume)   // the persistent work queue over the resident workgroups
             hipLaunchKernelGGL(kq, dim3(res), dim3(WAVE * WAVES_PER_BLOCK), smem, st, P0);
         else if (P0.team > 0)        // a split launch with team records: both phases on the team-capable build
             hipLaunchKernelGGL(kt, dim3(need_t > 0 ? need_t : 1u), dim3(WAVE * TEAM_WAVES), smem_t, st, P0);
@@ -4652,8 +4797,17 @@ void launch_solve(const KP& P0, size_t smem, hipStream_t st, unsigned* res_out)
     };
     // the team-capable build exists in fp64 only: in fp32 its different code rounded differently from the plain build's
     // (fp32 contraction / packing decisions depend on the surrounding code), so fp32 splits never make team records
-#define ALIP_GO(K) go(solve_kernel<N, K, R, false>, solve_kernel<N, K, R, true>, \
-                      solve_kernel<N, K, R, true, sizeof(R) == 8>)
+    // cfg.restoration = IPOPT: the restoration-capable builds, except for phase 1 of a split launch (records: a pending
+    // restoration is cut to phase 2); the query of the resident slots uses the lean work-queue build either way
+    const bool rs = P0.resto_ipopt && !(P0.ckpt && !P0.resume) && !res_out;
+#define ALIP_GO(K)                                                                                              \
+    do {                                                                                                        \
+        if (rs)                                                                                                 \
+            go(solve_kernel<N, K, R, false, false, true>, solve_kernel<N, K, R, true, false, true>,             \
+               solve_kernel<N, K, R, true, sizeof(R) == 8, true>);                                              \
+        else                                                                                                    \
+            go(solve_kernel<N, K, R, false>, solve_kernel<N, K, R, true>, solve_kernel<N, K, R, true, sizeof(R) == 8>); \
+    } while (0)
 #ifdef ALIP_DEV_ONLY_KSM   // dev builds for register reports (tools/regs.py): one row-step count only
     ALIP_GO(ALIP_DEV_ONLY_KSM);
 #else
@@ -4904,6 +5058,9 @@ struct Handle {
     };
     std::map<hipStream_t, SplitBuf> split;
     std::mutex split_mtx;
+    // lane program with cfg.restoration = IPOPT: per stream, the list of instances handed to the wave program (count +
+    // indices; grown to the largest batch seen, never freed before alipmpc_destroy)
+    std::map<hipStream_t, SplitBuf> redo;
     // launch timing: a ring of event pairs, so a re-record never targets an event still pending on the
     // stream (that serialises the host with the previous launch)
     static constexpr int NEV = 16;
@@ -5092,7 +5249,7 @@ int lane_slots_for(const alipmpc_cfg& c)
     return c.nc_max == 0 ? 0 : c.nc_max <= 5 ? 5 : 6;
 }
 
-size_t smem_bytes(const Handle* h, bool solve)
+size_t smem_bytes(const Handle* h, bool solve, int force_f64 = 0)
 {
     if (h->cfg.variant == ALIPMPC_VARIANT_DD) {
         int wsd = 0;
@@ -5105,7 +5262,7 @@ size_t smem_bytes(const Handle* h, bool solve)
         (void)solve;
         return sizeof(double) * ((size_t)KP_DOUBLES + (size_t)WAVES_PER_BLOCK * wsd);
     }
-    const bool f32 = solve && h->cfg.precision == ALIPMPC_PREC_FP32;
+    const bool f32 = solve && h->cfg.precision == ALIPMPC_PREC_FP32 && !force_f64;
     int wsd = 0;
     switch (h->N) {
 #define WSCASE(NN)                                                                                     \
@@ -5141,6 +5298,7 @@ KP make_kp(const Handle* h, long long B, bool solve)
     P.select_obs = c.select_obs;
     P.detour = c.detour;
     P.goal_abort = c.goal_singular == ALIPMPC_GOAL_SINGULAR_ABORT;
+    P.resto_ipopt = c.restoration == ALIPMPC_RESTORATION_IPOPT && c.variant != ALIPMPC_VARIANT_DD;
     P.tol = c.tol;
     P.acc_tol = c.acceptable_tol;
     P.q = c.q;
@@ -5202,9 +5360,48 @@ hipError_t launch(const Handle* h, bool solve, const KP& P, hipStream_t st, unsi
         if (res_out) return hipErrorInvalidValue;
         return launch_sweep(h->sweep_nc, h->cfg.variant == ALIPMPC_VARIANT_MODI, P, st);
     }
-    if (solve && h->lane_nct >= 0)
-        return f32 ? launch_lane_f32(h->lane_nct, h->cfg.variant == ALIPMPC_VARIANT_MODI, P, st, res_out)
-                   : launch_lane_f64(h->lane_nct, h->cfg.variant == ALIPMPC_VARIANT_MODI, P, st, res_out);
+    if (solve && h->lane_nct >= 0) {
+        const bool modi = h->cfg.variant == ALIPMPC_VARIANT_MODI;
+        if (res_out || !P.resto_ipopt)
+            return f32 ? launch_lane_f32(h->lane_nct, modi, P, st, res_out) : launch_lane_f64(h->lane_nct, modi, P, st, res_out);
+        KP P1 = P;
+        {
+            Handle* hm = const_cast<Handle*>(h);
+            std::lock_guard<std::mutex> lk(hm->split_mtx);
+            Handle::SplitBuf& rb = hm->redo[st];
+            const size_t need = sizeof(uint32_t) * (size_t)(P.B + 1);
+            if (rb.bytes < need) {
+                hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+                if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone)
+                    return hipErrorNotSupported;   // (a capture needs an uncaptured solve of that size on the stream first)
+                if (rb.p) {
+                    (void)hipStreamSynchronize(st);
+                    (void)hipFree(rb.p);
+                    rb.p = nullptr;
+                    rb.bytes = 0;
+                }
+                if (hipError_t e = hipMalloc(&rb.p, need)) return e;
+                rb.bytes = need;
+            }
+            P1.redo = (uint32_t*)rb.p;
+        }
+        // cfg.restoration = IPOPT: the lane program solves every instance whose line searches all succeed; an instance
+        // whose search fails is listed (P.redo) and solved from its start by the fp64 wave program's restoration-capable
+        // work queue, on the same stream (the same queue pair: the lane kernel's last wave resets it)
+        if (hipError_t e = hipMemsetAsync(P1.redo, 0, sizeof(uint32_t), st)) return e;
+        if (hipError_t e = f32 ? launch_lane_f32(h->lane_nct, modi, P1, st, nullptr)
+                               : launch_lane_f64(h->lane_nct, modi, P1, st, nullptr))
+            return e;
+        KP Q = P;
+        Q.redo = nullptr;
+        Q.order = reinterpret_cast<const int32_t*>(P1.redo + 1);
+        Q.bcount = P1.redo;
+        const size_t sm = smem_bytes(h, true, 1);
+        switch (h->N) {
+        case 3: return launch_lip_3(true, false, Q, sm, st, nullptr);
+        }
+        return hipErrorInvalidValue;
+    }
     switch (h->N) {
     case 1: return launch_lip_1(solve, f32, P, smem, st, res_out);
     case 2: return launch_lip_2(solve, f32, P, smem, st, res_out);
@@ -5331,6 +5528,11 @@ int alipmpc_create(const alipmpc_cfg* cfg, int device, void** handle)
         return ALIPMPC_EINVAL;
     if (cfg->precision != ALIPMPC_PREC_FP64 && cfg->precision != ALIPMPC_PREC_FP32) return ALIPMPC_EINVAL;
     if (cfg->program != ALIPMPC_PROGRAM_WAVE && cfg->program != ALIPMPC_PROGRAM_LANE) return ALIPMPC_EINVAL;
+    // enum fields: callers start from alipmpc_default_cfg (a struct filled by hand must set them to a defined value)
+    if (cfg->goal_singular != ALIPMPC_GOAL_SINGULAR_ZERO && cfg->goal_singular != ALIPMPC_GOAL_SINGULAR_ABORT)
+        return ALIPMPC_EINVAL;
+    if (cfg->restoration != ALIPMPC_RESTORATION_IPOPT && cfg->restoration != ALIPMPC_RESTORATION_SUBSTITUTE)
+        return ALIPMPC_EINVAL;
     // fp32 arithmetic is implemented for the LIP solve kernels (modi, sig_step)
     if (cfg->precision == ALIPMPC_PREC_FP32 && cfg->variant == ALIPMPC_VARIANT_DD) return ALIPMPC_EUNSUPPORTED;
     if (cfg->variant != ALIPMPC_VARIANT_MODI && cfg->variant != ALIPMPC_VARIANT_SIG_STEP &&
@@ -5483,7 +5685,17 @@ static void* split_buffer(Handle* h, hipStream_t st, size_t need, hipError_t& er
         // every buffer is kept until alipmpc_destroy (an eviction's hipFree synchronised the device and
         // could free a buffer another thread had just been handed); a stream beyond SPLIT_STREAMS runs the one-phase
         // form, which computes the same bits
-        if (h->split.size() >= Handle::SPLIT_STREAMS) return nullptr;
+        // (the closed loop's own group streams do not count: ADVICE r5 — cycling user streams would otherwise leave
+        // its episode groups on the one-phase form)
+        bool group = false;
+        for (int g = 0; g < Handle::MAXG; ++g) group |= st != nullptr && st == h->gst[g];
+        size_t users = 0;
+        for (auto& kv : h->split) {
+            bool gk = false;
+            for (int g = 0; g < Handle::MAXG; ++g) gk |= kv.first != nullptr && kv.first == h->gst[g];
+            users += gk ? 0 : 1;
+        }
+        if (!group && users >= Handle::SPLIT_STREAMS) return nullptr;
         Handle::SplitBuf sb;
         if ((err = hipMalloc(&sb.p, need)) != hipSuccess) return nullptr;
         sb.bytes = need;
@@ -6224,6 +6436,26 @@ int alipmpc_solve_slots(void* handle, int64_t* slots)
     return ALIPMPC_OK;
 }
 
+int alipmpc_lane_handoffs(void* handle, void* hip_stream, int64_t* count)
+{
+    Handle* h = (Handle*)handle;
+    if (!h || !count) return fail(h, ALIPMPC_EINVAL, "null argument");
+    *count = 0;
+    hipStream_t st = stream_of(h, hip_stream);
+    void* p = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(h->split_mtx);
+        auto it = h->redo.find(st);
+        if (it != h->redo.end()) p = it->second.p;
+    }
+    if (!p) return ALIPMPC_OK;
+    uint32_t c = 0;
+    if (hipStreamSynchronize(st) != hipSuccess || hipMemcpy(&c, p, sizeof(c), hipMemcpyDeviceToHost) != hipSuccess)
+        return fail(h, ALIPMPC_EHIP, "alipmpc_lane_handoffs: reading the hand-off count");
+    *count = c;
+    return ALIPMPC_OK;
+}
+
 int alipmpc_solve_launches(void* handle, int64_t B, int32_t* launches, int32_t* team)
 {
     Handle* h = (Handle*)handle;
@@ -6270,6 +6502,8 @@ void alipmpc_destroy(void* handle)
     if (h->stage) hipFree(h->stage);
     if (h->rstage) hipFree(h->rstage);
     for (auto& kv : h->split)
+        if (kv.second.p) hipFree(kv.second.p);
+    for (auto& kv : h->redo)
         if (kv.second.p) hipFree(kv.second.p);
     for (auto& pr : h->ev)
         for (hipEvent_t e : pr)

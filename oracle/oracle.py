@@ -273,10 +273,12 @@ def cl_uniform(seed, b, s, i, axis):
 
 
 def closed_loop_batch(cfg, x0, foot0, goal, leg, cir, nc, elp=None, ne=None, steps=8, f_cyc=40, kick=0.0, seed=0,
-                      nthreads=8):
+                      nthreads=8, jitter=False):
     """Oracle of alipmpc_closed_loop_batch (include/alipmpc.h): the reference driver's per-tick loop
     (main_sim_mpc.py:65-135; Logger.set_stf_head / gen_nex_foot_input, data_procs/logger_mpc.py:270-371) on an
-    ALIP plant, every solve by the C oracle."""
+    ALIP plant, every solve by the C oracle.  jitter (study only, tools/self_drift.py): every solve's returned plan —
+    the next tick's warm start — moved by one ulp (True) or by a relative amount (a float), the size of the difference
+    between two implementations' returned iterates."""
     N, n = cfg.N, 5 * cfg.N
     x = np.array(x0, np.float64).reshape(-1, 5).copy()
     B = len(x)
@@ -354,7 +356,8 @@ def closed_loop_batch(cfg, x0, foot0, goal, leg, cir, nc, elp=None, ne=None, ste
                             nthreads=nthreads)
             status[idx, s, i] = o["status"]
             iters[idx, s, i] = o["iters"]
-            plan[idx] = o["u"]
+            plan[idx] = (np.nextafter(o["u"], np.inf) if jitter is True else o["u"] * (1.0 + float(jitter))) if jitter \
+                else o["u"]
             has_plan[idx] = True
             hdv[idx, 0] = o["foot"][:, 2]
             xp = o["x_pred"]

@@ -149,7 +149,9 @@ def test_sup_learn_warm_start_chain(gpu_lib, golden, coracle, max_iter):
     ticks), every call warm-started from the previous call's plan, unshifted (logger_iml.py:333-342: guess =
     ravel(mpc_state_tar), the previous gen_control_test's x_mpc_tar = the GPU's u_out; [x_nex] x 3 on the first
     call).  Checked against the same chain through the C oracle (same interior point) and against the recorded
-    cyipopt footholds (the count reproduced to <= 1e-4 is recorded; cold starts reproduce 477 at max_iter 30)."""
+    cyipopt footholds (the count reproduced to <= 1e-4 is recorded).  r6: with IPOPT's restoration phase (the default,
+    cfg.restoration) the chain reproduces 532 / 538 of the 640 calls at max_iter 30 / 100, the oracle the same
+    (profiles/r6/resto); the rounds-1-5 substitute reproduced 479 — the bar is 520."""
     d = golden("g3_sup_learn")
     n = len(d["leg"])
     cs = d["cir_safe"]
@@ -178,7 +180,7 @@ def test_sup_learn_warm_start_chain(gpu_lib, golden, coracle, max_iter):
     _artifact(f"sup_learn_chain_{max_iter}.json", rec)
     assert agree[both].mean() >= 0.97, rec
     assert (sg == so).mean() >= 0.95, rec
-    assert (eg <= 1e-4).sum() >= 465, rec
+    assert (eg <= 1e-4).sum() >= 520, rec
 
 
 @pytest.mark.parametrize("variant,name", [(0, "modi"), (1, "sig_step")])
@@ -954,6 +956,21 @@ def _cl_drift_table(o, ref, F, tol=1e-4):
     return rows
 
 
+def _self_drift(tag):
+    """The oracle loop's own sensitivity for a closed-loop case (tools/self_drift.py, profiles/r6/parity/self_drift.json):
+    per statistic the smallest value over its fp64 perturbation rows (one ulp at the start, one ulp at every solve, the
+    tolerance at every solve) — the floor a GPU-vs-oracle bar is set against."""
+    import json
+    import os
+    fn = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "r6", "parity",
+                      "self_drift.json")
+    with open(fn) as fh:
+        cases = json.load(fh)["cases"]
+    rows = [cases[k] for k in (tag, tag + "_jitter", tag + "_toljitter") if k in cases]
+    return {k: min(r[k] for r in rows) for k in ("status_agree", "iters_within_1", "steps_to_goal_agree", "foot_le_1e-3",
+                                                  "foot_le_1e-4")}
+
+
 @pytest.mark.parametrize("variant,kick,program,prec", [(0, 0.0, 0, 0), (0, 0.05, 0, 0), (1, 0.05, 0, 0), (0, 0.05, 1, 0),
                                                        (0, 0.05, 1, 1)])
 def test_closed_loop_matches_oracle(gpu_lib, coracle, variant, kick, program, prec):
@@ -1013,26 +1030,19 @@ def test_closed_loop_matches_oracle(gpu_lib, coracle, variant, kick, program, pr
         np.testing.assert_allclose(o["x"][:, 0], x0, rtol=0, atol=0)
         assert np.array_equal(np.isnan(o["action"]).all(-1), o["status"] == gpu_lib.ROLLOUT_DONE)
         return
-    # tick level: a warm-started solve sitting on the tolerance boundary may take one iteration more or less
-    # (or, rarely, end on another status) than the oracle's
-    assert (o["status"] == ref["status"]).mean() >= 0.98
-    # (r5: 0.978-0.997 — one episode's warm starts sit on the tolerance boundary at iteration 29 / 30 tick after tick,
-    # a rounding-level decision; on identical inputs the kernel's iteration counts are within one of the oracle's on
-    # 99.99 % of the solves, test_closed_loop_same_inputs_match_oracle)
-    assert (np.abs(o["iters"] - ref["iters"]) <= 1).mean() >= 0.97
-    # episode level: the same number of steps to the goal
-    assert (o["steps_to_goal"] == ref["steps_to_goal"]).mean() >= 0.9
-    # touchdown footholds of steps whose last solve converged on both sides
+    # Each statistic against the oracle loop's OWN sensitivity (r6): the same episodes through the
+    # oracle twice, the second perturbed by rounding-size amounts (one ulp at the start, one ulp / the tolerance at
+    # every solve: tools/self_drift.py, profiles/r6/parity/self_drift.json); two loops that differ only by rounding
+    # drift apart that much, so the GPU-vs-oracle bar is that figure minus 0.03.
+    sd = _self_drift(tag)
+    gstat = {"status_agree": (o["status"] == ref["status"]).mean(),
+             "iters_within_1": (np.abs(o["iters"] - ref["iters"]) <= 1).mean(),
+             "steps_to_goal_agree": (o["steps_to_goal"] == ref["steps_to_goal"]).mean(),
+             "foot_le_1e-3": (err[conv] <= 1e-3).mean(), "foot_le_1e-4": (err[conv] <= 1e-4).mean()}
+    for k, v in gstat.items():
+        assert v >= sd[k] - 0.03, (k, v, sd[k])
     assert conv.sum() >= 0.4 * B * S
-    # (measured on MI355X, profiles/r3/parity: 0.89-0.99 of the converged touchdown footholds within 1e-4 of the
-    # oracle's, median ~2e-14; the rest are episodes that drifted after a rounding-level change of path:
-    # profiles/r4/parity/closed_loop_drift_*.json gives the tick where each of them leaves the oracle)
-    # (r5: 0.89-0.99 — see the 1e-4 bar below)
-    assert (err[conv] <= 1e-3).mean() >= 0.85 and np.median(err[conv]) <= 1e-6
-    # (r4 measured 0.90-0.99; r5's IPOPT scaling and barrier floor moved these chaotic statistics to 0.87-0.99: every
-    # drift still starts at an unconverged or iteration-count-differing tick (below), and the kernel / oracle agreement
-    # itself is measured on identical inputs by test_closed_loop_same_inputs_match_oracle)
-    assert (err[conv] <= 1e-4).mean() >= 0.85, (err[conv] <= 1e-4).mean()
+    assert np.median(err[conv]) <= 1e-6
     # every drift starts at an unconverged solve (iteration cap / infeasible: the returned iterate is path-dependent)
     # or where the iteration count differs (a warm start on the tolerance boundary), never inside a converged solve
     # that took the same iterations (r4 measurement: profiles/r4/parity/closed_loop_drift_*.json)

@@ -473,3 +473,82 @@ def test_nlp_scaling_semantics(coracle, variant):
                                  None, None, u0[None])
     assert rs["status"][0] == r["status"][0] and abs(int(rs["iters"][0]) - int(r["iters"][0])) <= 1
     assert np.abs(rs["u"][0] - r["u"][0]).max() <= 1e-6
+
+
+def _chain(coracle, d, restoration, max_iter=30):
+    """the 640 recorded calls as the warm-started chain the reference ran (logger_iml.py:333-342), C oracle"""
+    cc = coracle.default_cfg(0, 3, nc_max=6, ne_max=0, max_iter=max_iter)
+    cc.restoration = restoration
+    n = len(d["leg"])
+    feet, st, u = np.zeros((n, 3)), np.zeros(n, np.int32), d["u0"][0]
+    for i in range(n):
+        o = coracle.solve_batch(cc, d["x_nex"][i:i + 1], np.array([[10.0, 10.0]]), d["leg"][i:i + 1],
+                                d["cir_safe"][None], np.array([6]), np.zeros((1, 0, 5)), np.zeros(1), u[None])
+        feet[i], st[i], u = o["foot"][0], o["status"][0], o["u"][0]
+    return np.max(np.abs(feet[:, :2] - d["foot_logged"]), axis=1), st
+
+
+def test_restoration_phase_reproduces_recorded_calls(golden, coracle):
+    """IPOPT's feasibility restoration phase (cfg.restoration = IPOPT, the default; np_oracle._resto / alipmpc_oracle.c
+    oresto) against the rounds-1-5 substitute on the 640 recorded cyipopt calls of sup_learn replayed as the reference's
+    warm-started chain: the restoration phase reproduces >= 30 more recorded footholds (<= 1e-4) than the substitute and
+    loses none (measured 532 vs 479, profiles/r6/resto/resto_chain.json); the statuses the reference labels as
+    failures (2) stay the same rows' (its Infeasible_Problem_Detected is what the logs call a failed plan)."""
+    d = golden("g3_sup_learn")
+    e_ip, s_ip = _chain(coracle, d, 0)
+    e_sub, s_sub = _chain(coracle, d, 1)
+    r_ip, r_sub = e_ip <= 1e-4, e_sub <= 1e-4
+    assert r_ip.sum() >= 520 and r_sub.sum() >= 470, (r_ip.sum(), r_sub.sum())
+    assert r_ip.sum() >= r_sub.sum() + 30
+    assert not np.any(r_sub & ~r_ip), np.nonzero(r_sub & ~r_ip)[0]
+    assert ((s_ip == 2) == (s_sub == 2)).mean() >= 0.97
+
+
+def test_restoration_phase_numpy_and_c_agree(coracle):
+    """The numpy and C restatements of the restoration phase agree on a batch with infeasible scenes (cfg2's shape):
+    statuses equal, footholds within 1e-6 on >= 97 % (rounding-level differences in a nonconvex solve)."""
+    import alipmpc.scenes as scenes
+    B = 96
+    bt = scenes.make_batch(B, seed=0, n_cir=5, N=3)
+    cc = coracle.default_cfg(0, 3, nc_max=5, ne_max=0)
+    ref = coracle.solve_batch(cc, bt["x0"], bt["goal"], bt["leg"], bt["cir"], bt["nc"], np.zeros((B, 0, 5)),
+                              np.zeros(B), bt["u0"], nthreads=4)
+    assert (ref["restorations"] > 0).sum() >= 5   # the batch exercises the phase
+    feet, st = np.zeros((B, 3)), np.zeros(B, np.int32)
+    cfg = O.default_cfg(0, 3, nc_max=5, ne_max=0)
+    for i in range(B):
+        pr = O.Problem(cfg, bt["x0"][i], bt["goal"][i], bt["leg"][i], bt["cir"][i][:bt["nc"][i]], np.zeros((0, 5)))
+        u, st[i], _ = O.solve_footholds(pr, bt["u0"][i])
+        feet[i] = O.plan(pr, u)[1]
+    assert (st == ref["status"]).mean() >= 0.97
+    assert np.mean(np.max(np.abs(feet - ref["foot"]), axis=1) <= 1e-6) >= 0.97
+
+
+def test_restoration_phase_semantics():
+    """The restoration phase's own contract (np_oracle._resto): from the failed point it returns either a point the
+    original filter accepts with violation <= 0.9 theta_R ("ok"), a converged restoration problem with violation above
+    1e-4 ("infeasible"), or the iteration cap; the iterations it used are counted in the solve's total."""
+    import alipmpc.scenes as scenes
+    bt = scenes.make_batch(64, seed=0, n_cir=5, N=3)
+    cfg = O.default_cfg(0, 3, nc_max=5, ne_max=0)
+    seen = {}
+    orig = O._resto
+
+    def spy(prob, x, s, zl, zu, mu_o, cl, cu, hl, hu, filt_o, theta_R, orig_phi, it, max_iter, tol, stats):
+        r = orig(prob, x, s, zl, zu, mu_o, cl, cu, hl, hu, filt_o, theta_R, orig_phi, it, max_iter, tol, stats)
+        code, x1, s1, _, _, it1 = r
+        seen[code] = seen.get(code, 0) + 1
+        assert it1 >= it and it1 <= max_iter
+        c1 = prob.constraints(x1)
+        if code == "ok" and it1 > it:
+            th = float(np.abs(c1 - s1).sum())
+            assert th <= 0.9 * theta_R * (1 + 1e-12) or th <= 1e-12
+        return r
+    O._resto = spy
+    try:
+        for i in range(64):
+            pr = O.Problem(cfg, bt["x0"][i], bt["goal"][i], bt["leg"][i], bt["cir"][i][:bt["nc"][i]], np.zeros((0, 5)))
+            O.solve_footholds(pr, bt["u0"][i])
+    finally:
+        O._resto = orig
+    assert seen.get("ok", 0) >= 5, seen

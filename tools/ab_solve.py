@@ -10,7 +10,7 @@ if len(sys.argv) > 2 and sys.argv[1] == "--one":
     import alipmpc
     from alipmpc import scenes
     B, reps = int(os.environ.get("AB_B", "4096")), int(os.environ.get("AB_REPS", "30"))
-    s = alipmpc.Solver(alipmpc.default_cfg(0, nc_max=5, ne_max=0))
+    s = alipmpc.Solver(alipmpc.default_cfg(0, nc_max=5, ne_max=0, restoration=int(os.environ.get("AB_REST", "0"))))
     bt = scenes.make_batch(B, seed=0, n_cir=5)
     dev = torch.device("cuda", 0)
     inp = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in bt.items() if v is not None}

@@ -36,7 +36,7 @@ def _hash(paths, extra):
 
 def part_obj(k, src, extra):
     os.makedirs(CACHE, exist_ok=True)
-    key = _hash([src, B.INC, B.MATH, B.HDR], [*B.ARCH, *B.FLAGS, *extra, str(k)])
+    key = _hash([src, B.INC, B.MATH, B.RESTO, B.HDR], [*B.ARCH, *B.FLAGS, *extra, str(k)])
     o = os.path.join(CACHE, f"part{k}_{key}.o")
     if not os.path.exists(o):
         cmd = [B.HIPCC, *B.ARCH, *B.FLAGS, *extra, f"-DALIP_PART={k}", "-c", "-o", o + ".tmp", src]
