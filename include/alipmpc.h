@@ -140,10 +140,11 @@ typedef struct alipmpc_cfg {
                            only when it converges to a point of local infeasibility;
                            ALIPMPC_RESTORATION_SUBSTITUTE (1) — the rounds-1..5 substitute: the shortest trial step,
                            slacks reset onto c(u), filter reset, status 2 after 6 such events.  The DD variant always
-                           runs the substitute.  Wave program: split launches run the phase in their second launch
-                           (a failed search in the first cuts the instance there).  Lane program: an instance whose
-                           search fails is handed to the fp64 wave program, which solves it from its start (both
-                           precisions; alipmpc_lane_handoffs counts them). */
+                           runs the substitute.  fp64 wave program: split launches run the phase in their second
+                           launch (a failed search in the first cuts the instance there).  Lane program (both
+                           precisions) and fp32 wave program: an instance whose search fails is handed to the fp64
+                           wave program, which solves it from its start (alipmpc_lane_handoffs counts them); the fp64
+                           workspace must then fit the LDS too (alipmpc_create: ALIPMPC_EUNSUPPORTED otherwise). */
     int32_t reserved_;  /* zero */
 } alipmpc_cfg;
 
@@ -317,10 +318,10 @@ int alipmpc_solve_slots(void* handle, int64_t* slots);
  * Profiling tools use it to turn per-dispatch figures into per-solve ones.  No reference counterpart. */
 int alipmpc_solve_launches(void* handle, int64_t B, int32_t* launches, int32_t* team);
 
-/* Lane program with cfg.restoration = ALIPMPC_RESTORATION_IPOPT: the instances of the last solve on this stream whose
- * line search failed in the lane program and which were therefore solved, from their start, by the fp64 wave
- * program's restoration-capable work queue (IPOPT's restoration phase: DESIGN.md §2 item 4).  Synchronises the
- * stream.  0 for other programs / restoration modes.  No reference counterpart. */
+/* Lane program (either precision) or fp32 wave program with cfg.restoration = ALIPMPC_RESTORATION_IPOPT: the instances
+ * of the last solve on this stream whose line search failed in that program and which were therefore solved, from
+ * their start, by the fp64 wave program's restoration-capable work queue (IPOPT's restoration phase: DESIGN.md §2
+ * item 4).  Synchronises the stream.  0 for other programs / restoration modes.  No reference counterpart. */
 int alipmpc_lane_handoffs(void* handle, void* hip_stream, int64_t* count);
 
 /* The device program this handle's solves run (cfg.program): "solve_kernel<N,rows/4,type>" (one instance per

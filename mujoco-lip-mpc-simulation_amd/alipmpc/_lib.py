@@ -238,8 +238,8 @@ class Solver:
         return int(n.value), int(t.value)
 
     def lane_handoffs(self, stream=None):
-        """Instances of the last lane-program solve on `stream` (None: the handle's own stream, the host-pointer calls)
-        that were handed to the fp64 wave program for IPOPT's restoration phase (include/alipmpc.h)."""
+        """Instances of the last lane-program or fp32 wave-program solve on `stream` (None: the handle's own stream, the
+        host-pointer calls) that were handed to the fp64 wave program for IPOPT's restoration phase (include/alipmpc.h)."""
         v = ctypes.c_int64(0)
         st = None if stream is None else _stream_arg(stream)
         self._check(self._L.alipmpc_lane_handoffs(self._h, st, ctypes.byref(v)), "alipmpc_lane_handoffs")

@@ -2384,6 +2384,21 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* wsb, int wv, lo
         STAMP(9);
     }
     if (status != ST_RESTO) break;
+    if constexpr (sizeof(R) == 4) {   // fp32: the fp64 wave program solves this instance from its start (the
+        // stream's hand-off list, P.redo; launch() runs it after this launch).  The fp32 restoration phase took other
+        // paths than the oracle's on the tolerance edges, and fp32's one lean build keeps every launch form
+        // bit-identical.
+        if (!P.redo) {   // (the host always provides the list; no write without one)
+            status = 2;
+            break;
+        }
+        if (lane == 0) {
+            const uint32_t k = atomicAdd(P.redo, 1u);
+            P.redo[1 + k] = (uint32_t)b;
+        }
+        status = ST_CKPT;
+        break;
+    }
     // the failed point (this iteration counted) enters the filter — IPOPT's augmented filter, with the point's
     // violation (the same sum as the iteration's theta) and barrier function — then the restoration phase from it
     ++n_rest;
@@ -4799,14 +4814,19 @@ void launch_solve(const KP& P0, size_t smem, hipStream_t st, unsigned* res_out)
     // (fp32 contraction / packing decisions depend on the surrounding code), so fp32 splits never make team records
     // cfg.restoration = IPOPT: the restoration-capable builds, except for phase 1 of a split launch (records: a pending
     // restoration is cut to phase 2); the query of the resident slots uses the lean work-queue build either way
+    // (fp32 has the lean build only: a failed search hands the instance to the fp64 wave program)
     const bool rs = P0.resto_ipopt && !(P0.ckpt && !P0.resume) && !res_out;
 #define ALIP_GO(K)                                                                                              \
     do {                                                                                                        \
-        if (rs)                                                                                                 \
-            go(solve_kernel<N, K, R, false, false, true>, solve_kernel<N, K, R, true, false, true>,             \
-               solve_kernel<N, K, R, true, sizeof(R) == 8, true>);                                              \
-        else                                                                                                    \
-            go(solve_kernel<N, K, R, false>, solve_kernel<N, K, R, true>, solve_kernel<N, K, R, true, sizeof(R) == 8>); \
+        if constexpr (sizeof(R) == 8) {                                                                         \
+            if (rs)                                                                                             \
+                go(solve_kernel<N, K, R, false, false, true>, solve_kernel<N, K, R, true, false, true>,         \
+                   solve_kernel<N, K, R, true, true, true>);                                                    \
+            else                                                                                                \
+                go(solve_kernel<N, K, R, false>, solve_kernel<N, K, R, true>, solve_kernel<N, K, R, true, true>); \
+        } else {                                                                                                \
+            go(solve_kernel<N, K, R, false>, solve_kernel<N, K, R, true>, solve_kernel<N, K, R, true, false>);  \
+        }                                                                                                       \
     } while (0)
 #ifdef ALIP_DEV_ONLY_KSM   // dev builds for register reports (tools/regs.py): one row-step count only
     ALIP_GO(ALIP_DEV_ONLY_KSM);
@@ -5336,6 +5356,56 @@ int ksm_of(int rows)
     return 1 << 20;
 }
 
+// cfg.restoration = IPOPT, fp32 programs and the lane program: the stream's hand-off list ([0] = count, then the
+// instances), allocated outside a capture (a capture needs an uncaptured solve of that size on the stream first)
+static hipError_t redo_list(const Handle* h, hipStream_t st, long long B, uint32_t** out)
+{
+    Handle* hm = const_cast<Handle*>(h);
+    std::lock_guard<std::mutex> lk(hm->split_mtx);
+    Handle::SplitBuf& rb = hm->redo[st];
+    const size_t need = sizeof(uint32_t) * (size_t)(B + 1);
+    if (rb.bytes < need) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return hipErrorNotSupported;
+        if (rb.p) {
+            (void)hipStreamSynchronize(st);
+            (void)hipFree(rb.p);
+            rb.p = nullptr;
+            rb.bytes = 0;
+        }
+        if (hipError_t e = hipMalloc(&rb.p, need)) return e;
+        rb.bytes = need;
+    }
+    *out = (uint32_t*)rb.p;
+    return hipSuccess;
+}
+
+// the listed instances, solved from their start by the fp64 wave program's restoration-capable work queue (slot k
+// solves redo[1 + k], k < redo[0]) on the same stream
+static hipError_t launch_handoff(const Handle* h, const KP& P, const uint32_t* redo, hipStream_t st)
+{
+    KP Q = P;
+    Q.redo = nullptr;
+    Q.order = reinterpret_cast<const int32_t*>(redo + 1);
+    Q.bcount = redo;
+    Q.ckpt = nullptr;
+    Q.cont = nullptr;
+    Q.resume = 0;
+    Q.team = 0;
+    Q.ckpt_it = 0;
+    Q.ckpt_tr = 0;
+    const size_t sm = smem_bytes(h, true, 1);
+    switch (h->N) {
+    case 1: return launch_lip_1(true, false, Q, sm, st, nullptr);
+    case 2: return launch_lip_2(true, false, Q, sm, st, nullptr);
+    case 3: return launch_lip_3(true, false, Q, sm, st, nullptr);
+    case 4: return launch_lip_4(true, false, Q, sm, st, nullptr);
+    case 5: return launch_lip_5(true, false, Q, sm, st, nullptr);
+    case 6: return launch_lip_6(true, false, Q, sm, st, nullptr);
+    }
+    return hipErrorInvalidValue;
+}
+
 // res_out != null: no launch, report the resident workgroups of the solve kernel (0 for DD: no queue)
 hipError_t launch(const Handle* h, bool solve, const KP& P, hipStream_t st, unsigned* res_out = nullptr)
 {
@@ -5364,43 +5434,28 @@ hipError_t launch(const Handle* h, bool solve, const KP& P, hipStream_t st, unsi
         const bool modi = h->cfg.variant == ALIPMPC_VARIANT_MODI;
         if (res_out || !P.resto_ipopt)
             return f32 ? launch_lane_f32(h->lane_nct, modi, P, st, res_out) : launch_lane_f64(h->lane_nct, modi, P, st, res_out);
-        KP P1 = P;
-        {
-            Handle* hm = const_cast<Handle*>(h);
-            std::lock_guard<std::mutex> lk(hm->split_mtx);
-            Handle::SplitBuf& rb = hm->redo[st];
-            const size_t need = sizeof(uint32_t) * (size_t)(P.B + 1);
-            if (rb.bytes < need) {
-                hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-                if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone)
-                    return hipErrorNotSupported;   // (a capture needs an uncaptured solve of that size on the stream first)
-                if (rb.p) {
-                    (void)hipStreamSynchronize(st);
-                    (void)hipFree(rb.p);
-                    rb.p = nullptr;
-                    rb.bytes = 0;
-                }
-                if (hipError_t e = hipMalloc(&rb.p, need)) return e;
-                rb.bytes = need;
-            }
-            P1.redo = (uint32_t*)rb.p;
-        }
         // cfg.restoration = IPOPT: the lane program solves every instance whose line searches all succeed; an instance
         // whose search fails is listed (P.redo) and solved from its start by the fp64 wave program's restoration-capable
         // work queue, on the same stream (the same queue pair: the lane kernel's last wave resets it)
+        KP P1 = P;
+        if (hipError_t e = redo_list(h, st, P.B, &P1.redo)) return e;
         if (hipError_t e = hipMemsetAsync(P1.redo, 0, sizeof(uint32_t), st)) return e;
         if (hipError_t e = f32 ? launch_lane_f32(h->lane_nct, modi, P1, st, nullptr)
                                : launch_lane_f64(h->lane_nct, modi, P1, st, nullptr))
             return e;
-        KP Q = P;
-        Q.redo = nullptr;
-        Q.order = reinterpret_cast<const int32_t*>(P1.redo + 1);
-        Q.bcount = P1.redo;
-        const size_t sm = smem_bytes(h, true, 1);
-        switch (h->N) {
-        case 3: return launch_lip_3(true, false, Q, sm, st, nullptr);
-        }
-        return hipErrorInvalidValue;
+        return launch_handoff(h, P, P1.redo, st);
+    }
+    if (solve && f32 && P.resto_ipopt && !res_out && !P.redo) {
+        // the fp32 wave program, cfg.restoration = IPOPT: the same hand-off (solve_one lists an instance whose search
+        // fails).  Phase 1 of a split launch starts the list and phase 2 continues it; the fp64 work queue runs after
+        // the last launch of the solve.
+        KP P1 = P;
+        if (hipError_t e = redo_list(h, st, P.B, &P1.redo)) return e;
+        if (!P.resume)
+            if (hipError_t e = hipMemsetAsync(P1.redo, 0, sizeof(uint32_t), st)) return e;
+        if (hipError_t e = launch(h, true, P1, st)) return e;
+        if (P.ckpt && !P.resume) return hipSuccess;
+        return launch_handoff(h, P, P1.redo, st);
     }
     switch (h->N) {
     case 1: return launch_lip_1(solve, f32, P, smem, st, res_out);
@@ -5636,7 +5691,11 @@ int alipmpc_create(const alipmpc_cfg* cfg, int device, void** handle)
             }
         }
     }
-    if (smem_bytes(h, true) > 160 * 1024 || smem_bytes(h, false) > 160 * 1024) {
+    // (fp32 with cfg.restoration = IPOPT hands instances to the fp64 wave program: its workspace must fit as well)
+    const bool handoff = cfg->variant != ALIPMPC_VARIANT_DD && cfg->restoration == ALIPMPC_RESTORATION_IPOPT &&
+                         (cfg->precision == ALIPMPC_PREC_FP32 || h->lane_nct >= 0);
+    if (smem_bytes(h, true) > 160 * 1024 || smem_bytes(h, false) > 160 * 1024 ||
+        (handoff && smem_bytes(h, true, 1) > 160 * 1024)) {
         alipmpc_destroy(h);
         return ALIPMPC_EUNSUPPORTED;
     }

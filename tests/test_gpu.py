@@ -721,7 +721,9 @@ def test_factorisation_failure_returns_last_iterate(gpu_lib, coracle, variant, p
     selection is off) makes the KKT matrix non-finite, so the inertia correction cannot regularise it at
     the first iteration.  The instance must stop with status -3 after 0 iterations, as the C oracle does,
     returning the iterate from before the failing iteration bit for bit (= the max_iter = 0 output); the
-    other instances of the batch are unaffected."""
+    other instances of the batch are unaffected.  fp32 (cfg.restoration = IPOPT): the fp32 program's line search
+    fails on the non-finite step first and hands the instance to the fp64 program (include/alipmpc.h), so the
+    iterate is the fp64 program's max_iter = 0 output."""
     from alipmpc import scenes
     bt = scenes.make_batch(4, seed=3, n_cir=4)
     cir = bt["cir"].copy()
@@ -732,6 +734,9 @@ def test_factorisation_failure_returns_last_iterate(gpu_lib, coracle, variant, p
     s = gpu_lib.Solver(gpu_lib.default_cfg(variant, 3, **kw))
     o = s.solve(bt["x0"], bt["goal"], bt["leg"], cir, bt["nc"], u0=bt["u0"])
     assert o["status"][1] == -3 and o["iters"][1] == 0
+    if prec:
+        assert s.lane_handoffs() >= 1
+        kw.pop("precision")
     s0 = gpu_lib.Solver(gpu_lib.default_cfg(variant, 3, max_iter=0, **kw))
     o0 = s0.solve(bt["x0"], bt["goal"], bt["leg"], cir, bt["nc"], u0=bt["u0"])
     assert np.array_equal(o["u"][1], o0["u"][1]) and np.array_equal(o["foot"][1], o0["foot"][1])

@@ -91,7 +91,7 @@ def run(args):
     dev = torch.device("cuda", 0)
     B, N = 4096, 3
     bt = scenes.make_batch(B, seed=0, n_cir=5, N=N)
-    cfg = alipmpc.default_cfg(alipmpc.VARIANT_MODI, N, nc_max=5, ne_max=0)
+    cfg = alipmpc.default_cfg(alipmpc.VARIANT_MODI, N, nc_max=5, ne_max=0, restoration=args.restoration)
     s = alipmpc.Solver(cfg, device=0)
     buf = np.zeros((48 * 4096, 8), np.uint64)
     os.makedirs(args.out, exist_ok=True)
@@ -167,5 +167,6 @@ if __name__ == "__main__":
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "wst"))
     ap.add_argument("--cuts", type=int, nargs="*", default=[16])
     ap.add_argument("--no-closed-loop", action="store_true")
+    ap.add_argument("--restoration", type=int, default=0, help="cfg.restoration (0 IPOPT, 1 substitute)")
     a = ap.parse_args()
     build() if a.what == "build" else run(a)
