@@ -118,6 +118,8 @@ def parse():
                     help="threads for the all-cores CPU baseline (the GPU box allots 16)")
     ap.add_argument("--sweep-batch", type=int, default=65536, help="instances for the Jacobian-sweep roofline")
     ap.add_argument("--program", default=None, choices=["wave", "lane"], help="default: the config's")
+    ap.add_argument("--restoration", default="ipopt", choices=["ipopt", "substitute"],
+                    help="cfg.restoration: IPOPT's restoration phase (default, the reference's) or the r1-r5 substitute")
     ap.add_argument("--closed-loop-steps", type=int, default=1,
                     help="walking steps of the per-tick closed-loop figure (f_cyc = 40 solves each; 0 = skip)")
     return ap.parse_args()
@@ -158,6 +160,7 @@ def main():
     prec = {"precision": alipmpc.PREC_FP32} if fp32 else {}
     program = args.program or preset.get("program", "wave")
     prec["program"] = alipmpc.PROGRAM_LANE if program == "lane" else alipmpc.PROGRAM_WAVE
+    prec["restoration"] = alipmpc.RESTORATION_SUBSTITUTE if args.restoration == "substitute" else alipmpc.RESTORATION_IPOPT
     cfg = alipmpc.default_cfg(variant, N, nc_max=n_cir, ne_max=n_elp, **prec)
     solver = alipmpc.Solver(cfg, device=dev.index)
     weak = preset["per_gpu"] or args.batch is not None

@@ -177,7 +177,8 @@ enum RowType { R_VBX = 0, R_VBY, R_CIR, R_ELP, R_LEG, R_DTH, R_FEN, R_FENM, R_NO
 
 // ---- diagnostic phase timers (compiled only with -DALIP_STAMPS; never in the product build)
 #ifdef ALIP_STAMPS
-constexpr int NSTAMP = 10;
+constexpr int NSTAMP = 25;   // 0-9 solve_one's sections, 10-21 resto_wave's, 22 / 23 restoration calls / iterations,
+                             // 24 solve_one's re-evaluation after a restoration
 __device__ unsigned long long g_stamps[NSTAMP];
 #define STAMP_DECL unsigned long long st_acc[NSTAMP] = {}; unsigned long long st_t = __builtin_amdgcn_s_memtime();
 #define STAMP(i)                                                              \
@@ -193,10 +194,30 @@ __device__ unsigned long long g_stamps[NSTAMP];
         if (lane_id() == 0)                                                   \
             for (int i_ = 0; i_ < NSTAMP; ++i_) atomicAdd(&g_stamps[i_], st_acc[i_]); \
     } while (0)
+#define RSTAMP_DECL unsigned long long rs_acc[12] = {}; unsigned long long rs_t = __builtin_amdgcn_s_memtime();
+#define RSTAMP(i)                                                             \
+    do {                                                                      \
+        __builtin_amdgcn_sched_barrier(0);                                    \
+        unsigned long long t_ = __builtin_amdgcn_s_memtime();                 \
+        rs_acc[i] += t_ - rs_t;                                               \
+        rs_t = t_;                                                            \
+        __builtin_amdgcn_sched_barrier(0);                                    \
+    } while (0)
+#define RSTAMP_FLUSH(nit)                                                     \
+    do {                                                                      \
+        if (lane_id() == 0) {                                                 \
+            for (int i_ = 0; i_ < 12; ++i_) atomicAdd(&g_stamps[10 + i_], rs_acc[i_]); \
+            atomicAdd(&g_stamps[22], 1ull);                                   \
+            atomicAdd(&g_stamps[23], (unsigned long long)(nit));              \
+        }                                                                     \
+    } while (0)
 #else
 #define STAMP_DECL
 #define STAMP(i) do {} while (0)
 #define STAMP_FLUSH do {} while (0)
+#define RSTAMP_DECL
+#define RSTAMP(i) do {} while (0)
+#define RSTAMP_FLUSH(nit) do {} while (0)
 #endif
 
 // ---- diagnostic per-instance record of the wave program (compiled only with -DALIP_WSTAMP; never in the product
@@ -1624,6 +1645,7 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* wsb, int wv, lo
             // IPOPT's restoration phase from the failed point (the current iterate, slacks and multipliers; the
             // augmented filter; theta_R), resto_wave.inc; its iterate comes back through the workspace
             rpend = false;
+            STAMP(8);
             RELANE();
 #pragma unroll
             for (int q = 0; q < RPL; ++q) {
@@ -1669,6 +1691,7 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* wsb, int wv, lo
             f_cur = obj_sum<N, RPL>(cr, mr4);
             theta_ok = false;
             wave_sync();
+            STAMP(24);
             if (rcode == RSW_INFEASIBLE || rcode == RSW_FAILED) {   // Infeasible_Problem_Detected
                 status = 2;
                 break;
@@ -2525,8 +2548,9 @@ __device__ __forceinline__ void queue_exit(uint32_t* q)
 template <int KSM, class R, bool RSW = false>
 constexpr int solve_waves()
 {
-    // RSW: the restoration-capable build of the one-wave-per-instance form (split phase 2, one-phase launches): its
-    // instances run on lone waves, so it takes the registers of 2 waves per SIMD (fp32: 4) instead of spilling
+    // RSW: the restoration-capable builds (fp64; split phase 2, one-phase launches, the work queue and the hand-off
+    // queue) take the registers of 2 waves per SIMD instead of spilling: the phase-2 instances run on lone waves, and
+    // at 4 waves the work-queue build spilled 520 B/lane (r6)
     return 4 * KSM > WAVE ? ALIP_WAVES_RPL2
                           : (RSW ? (sizeof(R) == 4 ? 4 : ALIP_WAVES_RS) : (sizeof(R) == 4 ? ALIP_WAVES_F32 : ALIP_WAVES_RPL1));
 }
@@ -2541,7 +2565,7 @@ constexpr int solve_waves()
 // above the slots whole and in half-slot chunks and compares status, iters, u, foot, x_pred exactly), so an
 // instance's result does not depend on its batch or on the device's slot count.
 template <int N, int KSM, class R, bool ONE, bool TM = false, bool RS = false>
-__global__ __launch_bounds__(WAVE * (TM ? TEAM_WAVES : WAVES_PER_BLOCK), (solve_waves<KSM, R, RS && ONE>())) void solve_kernel(KP Pv)
+__global__ __launch_bounds__(WAVE * (TM ? TEAM_WAVES : WAVES_PER_BLOCK), (solve_waves<KSM, R, RS>())) void solve_kernel(KP Pv)
 {
     constexpr int WPB = TM ? TEAM_WAVES : WAVES_PER_BLOCK;   // waves per workgroup (team-capable: the team size)
     using D = Dim<N>;

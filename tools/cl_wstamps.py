@@ -128,6 +128,8 @@ def run(args):
              "phase2_instances": n2, "phase1": summarize(p1, tag=f"split {cut} phase 1"),
              "phase2": summarize(p2, tag=f"split {cut} phase 2") if n2 else None}
         res["split"][str(cut)] = r
+        os.makedirs(args.out, exist_ok=True)
+        np.save(os.path.join(args.out, f"split{cut}_records.npy"), rec)
         print(json.dumps({k: v for k, v in r.items() if k not in ("phase1", "phase2")}))
         print(json.dumps(r["phase1"]))
         print(json.dumps(r["phase2"]))
