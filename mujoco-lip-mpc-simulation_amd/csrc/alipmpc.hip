@@ -131,6 +131,10 @@ __host__ __device__ constexpr int ckpt_doubles(int rpl) { return WAVE * (CKPT_RO
 #define ALIP_SPLIT_IT 14   // (r5 sweep on cfg2: 12 / 13 / 14 / 15 / 16 / 18 / 20 = 0.58 / 0.59 / 0.537 / 0.55 / 0.543 / 0.545 / 0.55 ms)
 #endif
 constexpr int SPLIT_IT_DEFAULT = ALIP_SPLIT_IT;   // phase-1 iteration cap of the split launch (launch_solve)
+// with IPOPT's restoration phase (cfg.restoration, r6: a failed search in phase 1 is cut there, so the restoration
+// instances reach phase 2 earlier; sweep on cfg2: 12 / 13 / 14 / 15 / 16 / 17 / 18 / 20 = 0.636 / 0.630 / 0.646 /
+// 0.653 / 0.613 / 0.626 / 0.641 / 0.650 ms)
+constexpr int SPLIT_IT_DEFAULT_RESTO = 16;
 constexpr int SPLIT_TR_DEFAULT = 0;               // phase-1 trial cut of a cold solve (0 = off: no team records)
 constexpr int CL_SPLIT_IT_DEFAULT = 20;           // the closed loop's per-tick solves: phase-1 cap (r5: 16 / 18 / 20 / 22 /
                                                    // 24 = 23.7 / 22.95 / 22.7 / 22.8 / 23.6 ms per loop)
@@ -5696,7 +5700,8 @@ int alipmpc_create(const alipmpc_cfg* cfg, int device, void** handle)
             h->sweep_nc = h->cfg.nc_max;
         {   // split launch of one-wave-per-instance batches (ALIPMPC_SPLIT_IT=0 turns it off)
             const char* se = std::getenv("ALIPMPC_SPLIT_IT");
-            h->split_it = se ? std::atoi(se) : SPLIT_IT_DEFAULT;
+            h->split_it = se ? std::atoi(se)
+                             : (cfg->restoration == ALIPMPC_RESTORATION_IPOPT ? SPLIT_IT_DEFAULT_RESTO : SPLIT_IT_DEFAULT);
             if (h->split_it < 0 || h->split_it >= h->cfg.max_iter) h->split_it = 0;
             auto env_int = [](const char* name, int dflt) {
                 const char* t = std::getenv(name);
