@@ -1005,8 +1005,9 @@ static void phess(const oprob* P, const double* pv, const double* y_, double* Hp
 /* IPOPT's default NLP scaling (nlp_scaling_method = gradient-based, nlp_scaling_max_gradient = 100,
    nlp_scaling_min_value = 1e-8), evaluated at the user's starting point u0 in the reference's own variables: the
    objective is scaled by 100 / max|grad f(u0)| where that maximum exceeds 100.  Constraint rows would be scaled the
-   same way, but their gradients stay below 2 in u for these NLPs (tests/test_oracle.py), so every
-   dc_i is 1. */
+   same way, but their gradients stay below 4 in u on every benchmark scene (measured max 3.5, sig_step; DESIGN.md §2
+   item 9) and exceed 100 only with select_obs = 0 and large distant ellipses, where IPOPT would scale the row and this
+   build does not (a stated deviation: tests/test_oracle.py::test_row_scaling_region); every dc_i is 1. */
 static double obj_scaling(const oprob* P, const double* u0)
 {
     double g[OMAXV];

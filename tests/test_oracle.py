@@ -552,3 +552,35 @@ def test_restoration_phase_semantics():
     finally:
         O._resto = orig
     assert seen.get("ok", 0) >= 5, seen
+
+
+def test_row_scaling_region():
+    """IPOPT's gradient-based scaling would also scale a constraint row whose gradient at the starting point exceeds 100
+    (nlp_scaling_max_gradient): the build scales the objective only.  Pinned here:
+    (a) on the benchmark scene generators (cfg2 modi, cfg3 N = 5 with ellipses, sig_step with select_obs = 0) every row
+    gradient stays below 4 in the reference's u (measured max 3.5 over 512 instances each), so no row would be scaled;
+    (b) the region where the deviation applies exists and is flagged: a 4 x 5 m ellipse 25 m away with obstacle
+    selection off (select_obs = 0) has a row gradient of ~190, and ScaledProblem.rows_over_max_gradient reports it;
+    the same scene with the reference's modi selection drops the obstacle (no such row)."""
+    from dataclasses import replace
+    from alipmpc import scenes
+    for variant, N, n_elp in ((0, 3, 0), (0, 5, 5), (1, 3, 0)):
+        bt = scenes.make_batch(32, seed=0, n_cir=5, n_elp=n_elp, N=N)
+        o = O.default_cfg(variant, N, nc_max=5, ne_max=n_elp)
+        for i in range(32):
+            elp = bt["elp"][i][:bt["ne"][i]] if n_elp else np.zeros((0, 5))
+            pr = O.Problem(o, bt["x0"][i], bt["goal"][i], bt["leg"][i], bt["cir"][i][:bt["nc"][i]], elp)
+            fp = O.FootholdProblem(pr.split_copy())
+            sp = O.ScaledProblem(fp, fp.p_of_u(bt["u0"][i]))
+            assert sp.max_constraint_gradient < 4.0 and sp.rows_over_max_gradient == 0, (variant, N, i)
+    x0 = np.array([0.0, 0.0, 0.1, 0.0, 0.0])
+    elp = np.array([[25.0, 3.0, 4.0, 5.0, 0.3]])
+    over = {}
+    for so in (0, 1):
+        o = replace(O.default_cfg(0, 3, nc_max=0, ne_max=1), select_obs=so)
+        pr = O.Problem(o, x0, np.array([5.0, 0.5]), 1, np.zeros((0, 3)), elp)
+        fp = O.FootholdProblem(pr.split_copy())
+        sp = O.ScaledProblem(fp, fp.p_of_u(np.tile(x0, 3)))
+        over[so] = (sp.rows_over_max_gradient, sp.max_constraint_gradient)
+    assert over[0][0] >= 1 and over[0][1] > 100.0, over
+    assert over[1] == (0, over[1][1]) and over[1][1] < 4.0, over
