@@ -205,6 +205,52 @@ def test_solve_cfg2_batch_vs_oracle(gpu_lib, coracle):
     assert np.allclose(o["u"].reshape(-1, 3, 5), o["x_pred"], rtol=0, atol=0)
 
 
+@pytest.mark.parametrize("prec", [0, 1])
+def test_max_slots_n6_every_launch_form(gpu_lib, coracle, prec):
+    """alipmpc_create either rejects a shape (EINVAL: N * rows_per_step > 128; EUNSUPPORTED: a
+    workspace beyond the CU's 160 KB of LDS, or an fp32 / lane hand-off whose fp64 workspace does not fit) or every
+    launch of it succeeds.  N = 6 (the horizon limit) at the largest obstacle-slot count create accepts, half circles and
+    half ellipses: the one-wave split form (B below the resident slots), the work queue (B above them) and one
+    closed-loop tick must all launch, return finite iterates and valid statuses, and agree with the C oracle's statuses
+    on the instances compared (fp64: >= 90 %; fp32: the instance solved at all).  (r5a's N = 6 `EHIP invalid argument`
+    was a launch of the team-capable build whose workspaces exceeded 160 KB at N = 6 — DESIGN.md §3.1.)"""
+    from alipmpc import scenes
+    N = 6
+    kw = {"precision": gpu_lib.PREC_FP32} if prec else {}
+    found = None
+    for tot in range(24, 0, -1):
+        nc, ne = (tot + 1) // 2, tot // 2
+        try:
+            s = gpu_lib.Solver(gpu_lib.default_cfg(0, N, nc_max=nc, ne_max=ne, **kw))
+        except RuntimeError as e:
+            assert "EINVAL" in str(e) or "EUNSUPPORTED" in str(e), str(e)
+            continue
+        found = (nc, ne, s)
+        break
+    assert found is not None
+    nc, ne, s = found
+    assert nc + ne >= 8, (nc, ne)   # (the largest accepted shape is not a degenerate one)
+    slots = s.solve_slots()
+    valid = {0, 1, 2, -1, -2, -3, -13}
+    for B in (64, slots + 64):
+        bt = scenes.make_batch(B, seed=61 + B % 7, n_cir=nc, n_elp=ne, N=N)
+        o = s.solve(bt["x0"], bt["goal"], bt["leg"], bt["cir"], bt["nc"], bt["elp"], bt["ne"], u0=bt["u0"])
+        assert np.isfinite(o["u"]).all() and set(np.unique(o["status"])) <= valid, (B, np.unique(o["status"]))
+        if B == 64:
+            co = coracle.default_cfg(0, N, nc_max=nc, ne_max=ne)
+            if prec:
+                co.tol, co.acceptable_tol = s.cfg.tol, s.cfg.acceptable_tol
+            ref = coracle.solve_batch(co, bt["x0"][:32], bt["goal"][:32], bt["leg"][:32], bt["cir"][:32], bt["nc"][:32],
+                                      bt["elp"][:32], bt["ne"][:32], bt["u0"][:32])
+            agree = np.mean(o["status"][:32] == ref["status"])
+            print(f"N=6 nc={nc} ne={ne} prec={prec}: status agreement {agree:.3f}")
+            assert agree >= (0.9 if not prec else 0.75), agree
+    foot0 = o["foot"][:64, 0:2].copy()
+    cl = s.closed_loop(bt["x0"][:64], foot0, bt["goal"][:64], bt["leg"][:64].astype(np.int8), bt["cir"][:64],
+                       bt["nc"][:64], bt["elp"][:64], bt["ne"][:64], steps=1, f_cyc=2)
+    assert set(np.unique(cl["status"])) <= valid | {gpu_lib.ROLLOUT_DONE}
+
+
 # (N <= 3 with more than 16 obstacle slots: the Hessian blocks' second slot per lane, hess_blocks_lanes; no obstacle
 # slots at N <= 3: the 4-row-step J layout, solve_kernel<N, 4, ...>)
 @pytest.mark.parametrize("variant,N,n_cir,n_elp", [(1, 3, 4, 0), (0, 3, 3, 3), (0, 5, 5, 5), (0, 1, 2, 0),
