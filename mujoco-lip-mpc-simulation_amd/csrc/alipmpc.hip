@@ -97,7 +97,7 @@ struct KP {
     int team;               // split launch (team-capable build): phase 1 — team records on (ckpt_tr); phase 2 — team
                             // workgroups ahead of the single ones (each runs one team record on its 4 waves in lockstep,
                             // consecutive line-search trials per round)
-    double* ckpt;           // split launch: per-record loop state (ckpt_doubles(RPL) each)
+    double* ckpt;           // split launch: per-record loop state (ckpt_doubles(mo4) each)
     uint32_t* cont;         // split launch counters (CONT_*): single / team records, then the instance of record k
                             // (singles from k = 0 up, team record j at k = B - 1 - j)
     // solve outputs
@@ -125,8 +125,15 @@ constexpr int FAIL_GOAL = 1 << 16;   // solve_kernel's fail_it tag of a cfg.goal
 // split-launch record of one instance: per lane and row group the row state (slack, multipliers, inverse slack
 // distances, value, transcendentals, the 4 generator values), the filter entries (2 x 2) and the generator value
 // V[lane]; then 16 uniform values
+// Split record layout (r6: live state only): CKPT_ROW row vectors of the instance's mo4 rows
+// (value i of row r at i * mo4 + r), the filter (entry j at CK_FILT + j for theta, + 128 for phi; only the nf live
+// entries are written and read), the iterate V (NG <= 56 lanes) and 13 scalars.  cfg2 (mo4 = 40): 6.5 KB per record,
+// ~4.7 KB written and read per cut instance (r5: 8.8 KB, all 64 lanes of every vector).
 constexpr int CKPT_ROW = 12;
-__host__ __device__ constexpr int ckpt_doubles(int rpl) { return WAVE * (CKPT_ROW * rpl + 5) + 16; }
+__host__ __device__ constexpr int ck_filt(int mo4) { return CKPT_ROW * mo4; }
+__host__ __device__ constexpr int ck_vme(int mo4) { return CKPT_ROW * mo4 + 4 * WAVE; }
+__host__ __device__ constexpr int ck_scal(int mo4) { return CKPT_ROW * mo4 + 4 * WAVE + 56; }
+__host__ __device__ constexpr int ckpt_doubles(int mo4) { return CKPT_ROW * mo4 + 4 * WAVE + 56 + 16; }
 #ifndef ALIP_SPLIT_IT
 #define ALIP_SPLIT_IT 14   // (r5 sweep on cfg2: 12 / 13 / 14 / 15 / 16 / 18 / 20 = 0.58 / 0.59 / 0.537 / 0.55 / 0.543 / 0.545 / 0.55 ms)
 #endif
@@ -1547,34 +1554,41 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* wsb, int wv, lo
     if (rec >= 0) {
         // split launch, phase 2: the loop state at the top of iteration `it`, from the record phase 1 wrote (all
         // of it: values the loop could recompute are stored too, so no recomputation can round differently).
-        const double* rc = P.ckpt + rec * ckpt_doubles(RPL);
+        const double* rc = P.ckpt + rec * ckpt_doubles(mo4);
+        const double* sc = rc + ck_scal(mo4);
+        nf = rfl((int)sc[5]);
 #pragma unroll
         for (int q = 0; q < RPL; ++q) {
-            const double* rq = rc + WAVE * CKPT_ROW * q + lane;
-            sr[q] = ck_get<R>(rq[0]);
-            zl[q] = ck_get<R>(rq[WAVE]);
-            zu[q] = ck_get<R>(rq[2 * WAVE]);
-            idl[q] = ck_get<R>(rq[3 * WAVE]);
-            idu[q] = ck_get<R>(rq[4 * WAVE]);
-            cr[q] = ck_get<R>(rq[5 * WAVE]);
-            ra0[q] = ck_get<R>(rq[6 * WAVE]);
-            ra1[q] = ck_get<R>(rq[7 * WAVE]);
+            const int r = lane + WAVE * q;
+            if (r < mo4) {   // (rows r >= mo4 keep the prologue's values: no row there)
+                const double* rq = rc + r;
+                sr[q] = ck_get<R>(rq[0]);
+                zl[q] = ck_get<R>(rq[mo4]);
+                zu[q] = ck_get<R>(rq[2 * mo4]);
+                idl[q] = ck_get<R>(rq[3 * mo4]);
+                idu[q] = ck_get<R>(rq[4 * mo4]);
+                cr[q] = ck_get<R>(rq[5 * mo4]);
+                ra0[q] = ck_get<R>(rq[6 * mo4]);
+                ra1[q] = ck_get<R>(rq[7 * mo4]);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) rv[q][i] = ck_get<R>(rq[(8 + i) * WAVE]);
+                for (int i = 0; i < 4; ++i) rv[q][i] = ck_get<R>(rq[(8 + i) * mo4]);
+            }
         }
-        const double* rf = rc + WAVE * CKPT_ROW * RPL + lane;
-        fth0 = ck_get<R>(rf[0]);
-        fph0 = ck_get<R>(rf[WAVE]);
-        fth1 = ck_get<R>(rf[2 * WAVE]);
-        fph1 = ck_get<R>(rf[3 * WAVE]);
-        vme = lane < NG ? ck_get<R>(rf[4 * WAVE]) : R(0.0);
-        const double* sc = rc + WAVE * (CKPT_ROW * RPL + 5);
+        const double* rf = rc + ck_filt(mo4) + lane;   // (entries >= nf are never read by the filter tests)
+        if (lane < nf) {
+            fth0 = ck_get<R>(rf[0]);
+            fph0 = ck_get<R>(rf[2 * WAVE]);
+        }
+        if (lane + WAVE < nf) {
+            fth1 = ck_get<R>(rf[WAVE]);
+            fph1 = ck_get<R>(rf[3 * WAVE]);
+        }
+        vme = lane < NG ? ck_get<R>(rc[ck_vme(mo4) + lane]) : R(0.0);
         mu = uni(ck_get<R>(sc[0]));
         f_cur = uni(ck_get<R>(sc[1]));
         lsum_cur = uni(ck_get<R>(sc[2]));
         theta_c = uni(ck_get<R>(sc[3]));
         dw_last = uni(ck_get<R>(sc[4]));
-        nf = rfl((int)sc[5]);
         it0 = rfl((int)sc[6]);
         n_rest = rfl((int)sc[7]);
         fail_it = rfl((int)sc[8]);
@@ -1610,34 +1624,41 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* wsb, int wv, lo
             k = to_team ? (int)(P.B - 1 - (long long)atomicAdd(P.cont + CONT_TEAM, 1u))
                         : (int)atomicAdd(P.cont + CONT_SINGLE, 1u);
         k = rfl(k);
-        double* rc = P.ckpt + (long long)k * ckpt_doubles(RPL);
+        double* rc = P.ckpt + (long long)k * ckpt_doubles(mo4);
 #pragma unroll
         for (int q = 0; q < RPL; ++q) {
-            double* rq = rc + WAVE * CKPT_ROW * q + lane;
-            rq[0] = ck_put(sr[q]);
-            rq[WAVE] = ck_put(zl[q]);
-            rq[2 * WAVE] = ck_put(zu[q]);
-            rq[3 * WAVE] = ck_put(idl[q]);
-            rq[4 * WAVE] = ck_put(idu[q]);
-            rq[5 * WAVE] = ck_put(cr[q]);
-            rq[6 * WAVE] = ck_put(ra0[q]);
-            rq[7 * WAVE] = ck_put(ra1[q]);
+            const int r = lane + WAVE * q;
+            if (r < mo4) {
+                double* rq = rc + r;
+                rq[0] = ck_put(sr[q]);
+                rq[mo4] = ck_put(zl[q]);
+                rq[2 * mo4] = ck_put(zu[q]);
+                rq[3 * mo4] = ck_put(idl[q]);
+                rq[4 * mo4] = ck_put(idu[q]);
+                rq[5 * mo4] = ck_put(cr[q]);
+                rq[6 * mo4] = ck_put(ra0[q]);
+                rq[7 * mo4] = ck_put(ra1[q]);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) rq[(8 + i) * WAVE] = ck_put(rv[q][i]);
+                for (int i = 0; i < 4; ++i) rq[(8 + i) * mo4] = ck_put(rv[q][i]);
+            }
         }
-        double* rf = rc + WAVE * CKPT_ROW * RPL + lane;
-        rf[0] = ck_put(fth0);
-        rf[WAVE] = ck_put(fph0);
-        rf[2 * WAVE] = ck_put(fth1);
-        rf[3 * WAVE] = ck_put(fph1);
-        rf[4 * WAVE] = ck_put(vme);
+        double* rf = rc + ck_filt(mo4) + lane;
+        if (lane < nf) {
+            rf[0] = ck_put(fth0);
+            rf[2 * WAVE] = ck_put(fph0);
+        }
+        if (lane + WAVE < nf) {
+            rf[WAVE] = ck_put(fth1);
+            rf[3 * WAVE] = ck_put(fph1);
+        }
+        if (lane < NG) rc[ck_vme(mo4) + lane] = ck_put(vme);
         const double sv[13] = {ck_put(mu), ck_put(f_cur), ck_put(lsum_cur), ck_put(theta_c), ck_put(dw_last),
                                (double)nf, (double)it, (double)n_rest, (double)fail_it, (double)it_end,
                                theta_ok ? 1.0 : 0.0, rp ? 1.0 : 0.0, ck_put(theta_R)};
         double v = 0.0;
 #pragma unroll
         for (int i = 0; i < 13; ++i) v = lane == i ? sv[i] : v;
-        if (lane < 13) rc[WAVE * (CKPT_ROW * RPL + 5) + lane] = v;
+        if (lane < 13) rc[ck_scal(mo4) + lane] = v;
         if (lane == 0) P.cont[cont_hdr(P.B) + k] = (uint32_t)b;
     };
     R phi_R = R(0.0);
@@ -5804,8 +5825,7 @@ static hipError_t launch_solve(Handle* h, const KP& P, hipStream_t st, int split
     const long long slots = (long long)res * WAVES_PER_BLOCK;
     if (slots < P.B) return launch(h, true, P, st);   // the work-queue form
     // records for the slots, not for this B: the buffer of a stream never changes size
-    const size_t rpl = (size_t)((h->mo4 + WAVE - 1) / WAVE);
-    const size_t rec_bytes = ((size_t)slots * ckpt_doubles((int)rpl) * sizeof(double) + 255) & ~(size_t)255;
+    const size_t rec_bytes = ((size_t)slots * ckpt_doubles(h->mo4) * sizeof(double) + 255) & ~(size_t)255;
     const size_t hdr = (size_t)cont_hdr(slots);
     const size_t need = rec_bytes + (hdr + (size_t)slots) * sizeof(uint32_t);
     hipError_t berr = hipSuccess;
