@@ -301,6 +301,9 @@ def main():
                 "peak": peak,
                 "unit": "TFLOP/s",
                 "frac": achieved / peak,
+                # fp32 configs: both fractions (the lane program's fp32 build keeps its KKT system in fp64)
+                "frac_fp64_peak": achieved / FP64_PEAK_TFLOPS if fp32 else None,
+                "frac_fp32_peak": achieved / FP32_PEAK_TFLOPS if fp32 else None,
                 "traffic": traffic,
                 "valu_issue_frac": prof.get("valu_issue_frac"),
                 "active_issue_frac": prof.get("active_issue_frac"),

@@ -36,7 +36,43 @@ __global__ __launch_bounds__(128) void stream_kernel(const double2* __restrict__
         }
     }
 }
+
+// r6: the same bytes in the runtime fill's order — the grid as a whole streams each buffer front to
+// back: store instruction k of wave w writes 1 KiB slice k * waves + w, so the grid's concurrent stores hit consecutive
+// slices (few open DRAM pages) instead of one 124 KiB block per wave; 256-thread workgroups, up to 8 per CU (32 waves).
+__global__ __launch_bounds__(256) void fill_order_kernel(const double2* __restrict__ in, double2* __restrict__ out,
+                                                         long long n_in16, long long n_out16)
+{
+    const int lane = threadIdx.x & 63;
+    const long long w = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const long long waves = (long long)gridDim.x * 4;
+    double2 acc = make_double2(0.0, 0.0);
+    for (long long e = w * 64 + lane; e < n_in16; e += waves * 64) {
+        const double2 v = in[e];
+        acc.x += v.x;
+        acc.y += v.y;
+    }
+#pragma unroll 4
+    for (long long e = w * 64 + lane; e < n_out16; e += waves * 64) out[e] = make_double2(acc.x + (double)e, acc.y);
+}
 }  // namespace
+
+extern "C" int fill_order_launch(const void* in, void* out, long long B, int grid, void* stream)
+{
+    hipLaunchKernelGGL(fill_order_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const double2*)in,
+                       (double2*)out, B * 304 / 16, B * 3968 / 16);
+    return (int)hipGetLastError();
+}
+
+extern "C" int fill_order_resident(int* blocks)
+{
+    int per_cu = 0, dev = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fill_order_kernel, 256, 0) != hipSuccess) return -1;
+    if (hipGetDevice(&dev) != hipSuccess) return -1;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return -1;
+    *blocks = per_cu * cus;
+    return 0;
+}
 
 extern "C" int ceiling_launch(const void* in, void* out, long long B, int grid, void* stream)
 {

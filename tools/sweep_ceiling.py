@@ -58,6 +58,42 @@ def main():
     byts = B * (304 + 3968)
     rep = {"kernel": "stream_kernel (tools/sweep_ceiling.hip)", "batch": B, "grid": blocks.value, "ms": ms,
            "bytes": byts, "GBs": byts / (ms * 1e-3) / 1e9, "frac_of_8TBs": byts / (ms * 1e-3) / 8e12}
+    # the fill's order (r6): the same bytes streamed front to back by the whole grid, 8 workgroups of 4 waves per CU
+    fb = ctypes.c_int(0)
+    assert L.fill_order_resident(ctypes.byref(fb)) == 0
+
+    def launch_f():
+        rc = L.fill_order_launch(ctypes.c_void_p(inp.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                                 ctypes.c_longlong(B), fb.value, sp)
+        assert rc == 0, rc
+    for _ in range(3):
+        launch_f()
+    torch.cuda.synchronize(dev)
+    if hasattr(torch.cuda, "_sleep"):
+        with torch.cuda.stream(st):
+            torch.cuda._sleep(int(2e7))
+    a.record(st)
+    for _ in range(reps):
+        launch_f()
+    b.record(st)
+    torch.cuda.synchronize(dev)
+    fms = a.elapsed_time(b) / reps
+    rep.update({"fill_order_kernel_grid": fb.value, "fill_order_ms": fms, "fill_order_GBs": byts / (fms * 1e-3) / 1e9,
+                "fill_order_frac_of_8TBs": byts / (fms * 1e-3) / 8e12})
+    # and torch's own fill of the output buffer (the runtime's fill kernel), the same way
+    for _ in range(2):
+        out.fill_(1.0)
+    torch.cuda.synchronize(dev)
+    if hasattr(torch.cuda, "_sleep"):
+        with torch.cuda.stream(st):
+            torch.cuda._sleep(int(2e7))
+    a.record(st)
+    for _ in range(reps):
+        out.fill_(1.0)
+    b.record(st)
+    torch.cuda.synchronize(dev)
+    zms = a.elapsed_time(b) / reps
+    rep.update({"torch_fill_out_ms": zms, "torch_fill_out_GBs": B * 3968 / (zms * 1e-3) / 1e9})
     import bench
     import alipmpc
     from alipmpc import scenes
