@@ -188,8 +188,9 @@ enum RowType { R_VBX = 0, R_VBY, R_CIR, R_ELP, R_LEG, R_DTH, R_FEN, R_FENM, R_NO
 
 // ---- diagnostic phase timers (compiled only with -DALIP_STAMPS; never in the product build)
 #ifdef ALIP_STAMPS
-constexpr int NSTAMP = 25;   // 0-9 solve_one's sections, 10-21 resto_wave's, 22 / 23 restoration calls / iterations,
-                             // 24 solve_one's re-evaluation after a restoration
+constexpr int NSTAMP = 26;   // 0-9 solve_one's sections, 10-21 resto_wave's, 22 / 23 restoration calls / iterations,
+                             // 24 solve_one's re-evaluation after a restoration, 25 the restoration call as solve_one
+                             // sees it (hand-over to LDS + resto_wave)
 __device__ unsigned long long g_stamps[NSTAMP];
 #define STAMP_DECL unsigned long long st_acc[NSTAMP] = {}; unsigned long long st_t = __builtin_amdgcn_s_memtime();
 #define STAMP(i)                                                              \
@@ -1685,6 +1686,7 @@ __device__ __forceinline__ void solve_one(const KP& P0, R* G, R* wsb, int wv, lo
             if (lane < NG) w.V[lane] = vme;
             wave_sync();
             const int rr = rfl(resto_wave<N, KSM, R>(wv, fth0, fph0, fth1, fph1, nf, mu, theta_R, it));
+            STAMP(25);
             const int rcode = rr & 15;
             it = rr >> 4;
             RELANE();

@@ -27,7 +27,7 @@ RES = ["entry", "orig check", "coef+J^Ty", "err+mu", "weights", "hess blocks", "
 bt = scenes.make_batch(4096, seed=0, n_cir=5)
 for rest in (alipmpc.RESTORATION_IPOPT, alipmpc.RESTORATION_SUBSTITUTE):
     s = alipmpc.Solver(alipmpc.default_cfg(0, nc_max=5, ne_max=0, restoration=rest))
-    buf = np.zeros(25, np.uint64)
+    buf = np.zeros(26, np.uint64)
     s.solve(bt["x0"], bt["goal"], bt["leg"], bt["cir"], bt["nc"], u0=bt["u0"])
     L.alipmpc_dbg_stamps(buf.ctypes.data_as(ctypes.c_void_p), 1)
     o = s.solve(bt["x0"], bt["goal"], bt["leg"], bt["cir"], bt["nc"], u0=bt["u0"])
@@ -39,6 +39,7 @@ for rest in (alipmpc.RESTORATION_IPOPT, alipmpc.RESTORATION_SUBSTITUTE):
           f"restoration iterations {rits}; wave cycles per regular iteration {main.sum() / max(1, its - rits):.0f}")
     for n, v in zip(MAIN, main):
         print(f"   {n:14s} {v / max(1, its - rits):10.0f} cyc/iter")
+    print(f"   {'resto call':14s} {float(buf[25]) / max(1, calls):10.0f} cyc/call (solve_one's view)")
     print(f"   {'post-resto':14s} {float(buf[24]) / max(1, calls):10.0f} cyc/call")
     if calls:
         r = buf[10:22].astype(float)
